@@ -1,0 +1,559 @@
+// et_lookup.hip — forward gather kernels for gfx950 (included by embtab.hip).
+//
+// Replaces the reference's CPU kernels (darchr/EmbeddingTables.jl):
+//   lookup_generic! / lookup_static!        src/lookup.jl:51-182
+//   maplookup!(::PreallocationStrategy)     src/lookup.jl:316-371
+//
+// Design:
+//   * one lane GROUP per output bag; a group is the LPR = min(64, row_bytes/16) lanes
+//     that together hold one embedding row as 16-byte vectors, so D = 128 fp32
+//     (512 B) is a half-wave and one wave-instruction moves two rows (1 KiB);
+//   * the bag's index list is read once, coalesced, by the group's lanes and
+//     broadcast with a lane shuffle (ds_bpermute), so row addresses never wait on a
+//     second global load;
+//   * U rows per group are issued before any is consumed (U * 1 KiB per wave in
+//     flight), then accumulated strictly in pool order starting from the first
+//     row — the reference's summation order, so fp32 results are bit-identical;
+//   * a workgroup (4 waves) owns a chunk of consecutive bags of ONE table; the
+//     grid enumerates (table, chunk) items table-fastest, like the reference's
+//     `_divrem_index(k, ntables)` work queue (src/lookup.jl:351-355);
+//   * descriptors travel by value in the kernel-argument segment (no device
+//     allocation, hipGraph-capturable).
+#include "et_common.h"
+
+namespace et {
+
+struct LookupPack {
+    et_lookup_desc d[ET_MAX_TABLES_PER_LAUNCH];
+};
+
+// Geometry of the vector path for element type T and feature size D.
+template <typename T, int D>
+struct VecGeom {
+    static constexpr int N = 16 / (int)sizeof(T);     // elements per 16-B vector
+    static constexpr int VPR = D / N;                 // vectors per row
+    static constexpr int LPR = VPR < 64 ? VPR : 64;   // lanes per group (one row)
+    static constexpr int NV = VPR / LPR;              // vectors per lane per row
+    static constexpr int GPW = 64 / LPR;              // groups (bags) per wave
+    static constexpr int U = NV >= 8 ? 1 : 8 / NV;    // default rows in flight per group
+    static_assert(D % N == 0, "row must be whole vectors");
+    static_assert(VPR <= 64 ? (64 % VPR == 0) : (VPR % 64 == 0), "unsupported row size");
+};
+
+template <typename T, int N>
+__device__ __forceinline__ void unpack16(u32x4 v, T (&x)[N]) {
+    static_assert(N * sizeof(T) == 16, "");
+    __builtin_memcpy(x, &v, 16);
+}
+
+template <typename T, int N>
+__device__ __forceinline__ u32x4 pack16(const T (&x)[N]) {
+    u32x4 v;
+    __builtin_memcpy(&v, x, 16);
+    return v;
+}
+
+// Issue UU row loads of one bag (slots i0 .. i0+UU-1 of the current index chunk,
+// all valid), then add them to the accumulator in slot order.  Straight-line code:
+// every load is issued before the first add waits, so UU rows per group are in
+// flight (the waitcnt pass counts vmcnt down through the adds).
+template <typename T, typename A, int D, int UU>
+__device__ __forceinline__ void load_add(const T* __restrict__ table, uint64_t ld_table,
+                                         uint64_t nrows, long long my, int gbase, int sub,
+                                         int i0, bool first_batch,
+                                         A (&acc)[VecGeom<T, D>::NV][VecGeom<T, D>::N],
+                                         bool& bad) {
+    using G = VecGeom<T, D>;
+    constexpr int N = G::N, LPR = G::LPR, NV = G::NV;
+    uint64_t off[UU];
+    bool ok[UU];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const long long r = __shfl(my, gbase + i0 + u, 64);
+        const uint64_t row = (uint64_t)(r - 1);
+        ok[u] = row < nrows;
+        off[u] = ok[u] ? row * ld_table : 0;
+    }
+    u32x4 buf[UU][NV];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(table + off[u]) + sub;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) buf[u][v] = src[v * LPR];
+    }
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        bad |= !ok[u];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            T x[N];
+            unpack16<T, N>(ok[u] ? buf[u][v] : u32x4{0u, 0u, 0u, 0u}, x);
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                if (u == 0)
+                    acc[v][k] = first_batch ? A(x[k]) : A(acc[v][k] + A(x[k]));
+                else
+                    acc[v][k] = A(acc[v][k] + A(x[k]));
+            }
+        }
+    }
+}
+
+// Pooled sum of one bag by one lane group (vector path).
+//   ip  : the bag's index list (1-based), `pool` entries
+//   out : the bag's output column
+//   sub : lane within the group, gbase : first lane of the group in the wave
+// Accumulation is acc = row(I[1]); acc += row(I[i]) for i = 2..P, element-wise and in
+// order (src/lookup.jl:139-146), so fp32/fp64/int results equal the reference bit
+// for bit; F16 rounds after every add (Julia Float16 `+`) unless A = float.
+template <typename T, typename A, int D, int U, bool NT>
+__device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, int64_t ld_table,
+                                            int64_t nrows, const int64_t* __restrict__ ip,
+                                            int pool, T* __restrict__ out, int sub, int gbase) {
+    using G = VecGeom<T, D>;
+    constexpr int N = G::N, LPR = G::LPR, NV = G::NV;
+    A acc[NV][N];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[v][k] = A(0);
+    bool bad = false;
+    const uint64_t ldt = (uint64_t)ld_table, nr = (uint64_t)nrows;
+
+    for (int c0 = 0; c0 < pool; c0 += LPR) {
+        const int cnt = pool - c0 < LPR ? pool - c0 : LPR;
+        // One coalesced read of (up to) LPR indices of this bag; lanes past the end
+        // re-read the last one so that no lane is masked off.
+        const long long my = (long long)ip[c0 + (sub < cnt ? sub : cnt - 1)];
+        int i0 = 0;
+        for (; i0 + U <= cnt; i0 += U)
+            load_add<T, A, D, U>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+        if constexpr (U > 4) {
+            if (cnt - i0 >= 4) {
+                load_add<T, A, D, 4>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+                i0 += 4;
+            }
+        }
+        if constexpr (U > 2) {
+            if (cnt - i0 >= 2) {
+                load_add<T, A, D, 2>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+                i0 += 2;
+            }
+        }
+        if (cnt - i0 >= 1)
+            load_add<T, A, D, 1>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+    }
+    if (bad) note_oob();
+    u32x4* o = reinterpret_cast<u32x4*>(out) + sub;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        T y[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) y[k] = T(acc[v][k]);
+        store16<NT>(o + v * LPR, pack16<T, N>(y));
+    }
+}
+
+// Pooled-sum kernel, vector path: grid = ntables * nchunks workgroups of 256.
+template <typename T, typename A, int D, int U, bool NT>
+__global__ __launch_bounds__(256) void k_pooled_vec(LookupPack pack, int ntables, int64_t batch,
+                                                    T* __restrict__ dst, int64_t ld_dst,
+                                                    int rounds) {
+    using G = VecGeom<T, D>;
+    const int64_t item = blockIdx.x;
+    const int t = (int)(item % ntables);
+    const int64_t chunk = item / ntables;
+    const et_lookup_desc& d = pack.d[t];
+    const T* table = reinterpret_cast<const T*>(d.table);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / G::LPR, sub = lane % G::LPR;
+    const int64_t per_round = 4 * G::GPW;
+    int64_t bag = chunk * per_round * rounds + wave * G::GPW + g;
+    for (int r = 0; r < rounds; ++r, bag += per_round) {
+        if (bag >= batch) break;
+        bag_sum_vec<T, A, D, U, NT>(table, d.ld_table, d.nrows, d.idx + bag * d.ld_idx, d.pool,
+                                 dst + bag * ld_dst + d.dst_row_off, sub, g * G::LPR);
+    }
+}
+
+// Non-reducing gather (bit copy) of RB-byte rows: each group moves U rows at once.
+template <int RB, bool NT>
+__global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables, int64_t batch,
+                                                    char* __restrict__ dst, int64_t ld_dst_b,
+                                                    int es, int rounds) {
+    constexpr int VPR = RB / 16;
+    constexpr int LPR = VPR < 64 ? VPR : 64;
+    constexpr int NV = VPR / LPR;
+    constexpr int GPW = 64 / LPR;
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
+    static_assert(VPR <= 64 ? (64 % VPR == 0) : (VPR % 64 == 0), "unsupported row size");
+
+    const int64_t item = blockIdx.x;
+    const int t = (int)(item % ntables);
+    const int64_t chunk = item / ntables;
+    const et_lookup_desc& d = pack.d[t];
+    const char* table = reinterpret_cast<const char*>(d.table);
+    const int64_t ld_b = d.ld_table * es;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / LPR, sub = lane % LPR;
+    const int64_t per_round = 4 * GPW;
+    const int64_t per_block = per_round * U * rounds;
+    int64_t bag0 = chunk * per_block + wave * GPW + g;
+    for (int r = 0; r < rounds; ++r, bag0 += per_round * U) {
+        if (bag0 >= batch) break;
+        uint64_t off[U];
+        bool okv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int64_t bag = bag0 + u * per_round;
+            bag = bag < batch ? bag : batch - 1;  // keep every lane active
+            const uint64_t row = (uint64_t)(d.idx[bag * d.ld_idx] - 1);
+            okv[u] = row < (uint64_t)d.nrows;
+            off[u] = okv[u] ? row * (uint64_t)ld_b : 0;
+        }
+        u32x4 buf[U][NV];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const u32x4* src = reinterpret_cast<const u32x4*>(table + off[u]) + sub;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) buf[u][v] = src[v * LPR];
+        }
+        bool bad = false;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t bag = bag0 + u * per_round;
+            if (bag < batch) {
+                bad |= !okv[u];
+                u32x4* o =
+                    reinterpret_cast<u32x4*>(dst + bag * ld_dst_b + d.dst_row_off * es) + sub;
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    store16<NT>(o + v * LPR, okv[u] ? buf[u][v] : u32x4{0u, 0u, 0u, 0u});
+            }
+        }
+        if (bad) note_oob();
+    }
+}
+
+// Generic path: any feature size / alignment / per-table dims.  One wave per bag,
+// lanes stride over the features, pool order sequential per feature.
+template <typename T, typename A, bool NT>
+__global__ __launch_bounds__(256) void k_pooled_generic(LookupPack pack, int ntables,
+                                                        int64_t batch, T* __restrict__ dst,
+                                                        int64_t ld_dst) {
+    constexpr int K = 4;
+    const int64_t item = blockIdx.x;
+    const int t = (int)(item % ntables);
+    const int64_t chunk = item / ntables;
+    const et_lookup_desc& d = pack.d[t];
+    const T* table = reinterpret_cast<const T*>(d.table);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t bag = chunk * 4 + wave;
+    if (bag >= batch) return;
+    const int64_t* ip = d.idx + bag * d.ld_idx;
+    T* out = dst + bag * ld_dst + d.dst_row_off;
+    const int dim = d.dim, pool = d.pool;
+    for (int f0 = 0; f0 < dim; f0 += 64 * K) {
+        A acc[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc[k] = A(0);
+        for (int i = 0; i < pool; ++i) {
+            uint64_t row = (uint64_t)(ip[i] - 1);
+            const bool ok = row < (uint64_t)d.nrows;
+            if (!ok && lane == 0 && f0 == 0) note_oob();
+            row = ok ? row : 0;
+            const T* src = table + row * (uint64_t)d.ld_table;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int f = f0 + lane + 64 * k;
+                if (f < dim) {
+                    const T x = ok ? src[f] : T(0);
+                    acc[k] = i == 0 ? A(x) : A(acc[k] + A(x));
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int f = f0 + lane + 64 * k;
+            if (f < dim) store_scalar<NT>(out + f, T(acc[k]));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host dispatch
+// ---------------------------------------------------------------------------
+
+constexpr int kVecDims[] = {16, 32, 64, 128, 256, 512};
+
+inline bool vec_dim_ok(int D) {
+    for (int x : kVecDims)
+        if (x == D) return true;
+    return false;
+}
+
+inline bool gather_rb_ok(int64_t rb) {
+    return rb == 32 || rb == 64 || rb == 128 || rb == 256 || rb == 512 || rb == 1024 ||
+           rb == 2048 || rb == 4096;
+}
+
+// Bags per workgroup round for the vector path.
+inline int rounds_for(int64_t batch, int64_t bags_per_round, int ntables) {
+    // Aim for >= ~8 workgroups per CU (2048) before making workgroups longer.
+    int64_t blocks1 = (batch + bags_per_round - 1) / bags_per_round * ntables;
+    int rounds = 1;
+    while (rounds < 8 && blocks1 / (rounds * 2) >= 4096) rounds *= 2;
+    return rounds;
+}
+
+template <typename T, typename A, int D, bool NT>
+int launch_pooled_vec(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
+                      hipStream_t s) {
+    using G = VecGeom<T, D>;
+    const int64_t per_round = 4 * G::GPW;
+    const int rounds = rounds_for(batch, per_round, n);
+    const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
+    const int64_t grid = nchunks * n;
+    if (grid <= 0) return ET_OK;
+    if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+    hipLaunchKernelGGL((k_pooled_vec<T, A, D, G::U, NT>), dim3((unsigned)grid), dim3(256), 0, s, pack,
+                       n, batch, reinterpret_cast<T*>(dst), ld_dst, rounds);
+    ET_LAUNCH_CHECK("k_pooled_vec");
+    return ET_OK;
+}
+
+template <int RB, bool NT>
+int launch_gather_rb(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
+                     int es, hipStream_t s) {
+    constexpr int VPR = RB / 16;
+    constexpr int LPR = VPR < 64 ? VPR : 64;
+    constexpr int NV = VPR / LPR;
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
+    const int64_t per_round = 4 * (64 / LPR) * U;
+    const int rounds = rounds_for(batch, per_round, n);
+    const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
+    const int64_t grid = nchunks * n;
+    if (grid <= 0) return ET_OK;
+    if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+    hipLaunchKernelGGL((k_gather_vec<RB, NT>), dim3((unsigned)grid), dim3(256), 0, s, pack, n,
+                       batch, reinterpret_cast<char*>(dst), ld_dst * es, es, rounds);
+    ET_LAUNCH_CHECK("k_gather_vec");
+    return ET_OK;
+}
+
+template <bool NT>
+int launch_gather(const LookupPack& pack, int n, int64_t rb, int64_t batch, void* dst,
+                  int64_t ld_dst, int es, hipStream_t s) {
+    switch (rb) {
+        case 32: return launch_gather_rb<32, NT>(pack, n, batch, dst, ld_dst, es, s);
+        case 64: return launch_gather_rb<64, NT>(pack, n, batch, dst, ld_dst, es, s);
+        case 128: return launch_gather_rb<128, NT>(pack, n, batch, dst, ld_dst, es, s);
+        case 256: return launch_gather_rb<256, NT>(pack, n, batch, dst, ld_dst, es, s);
+        case 512: return launch_gather_rb<512, NT>(pack, n, batch, dst, ld_dst, es, s);
+        case 1024: return launch_gather_rb<1024, NT>(pack, n, batch, dst, ld_dst, es, s);
+        case 2048: return launch_gather_rb<2048, NT>(pack, n, batch, dst, ld_dst, es, s);
+        case 4096: return launch_gather_rb<4096, NT>(pack, n, batch, dst, ld_dst, es, s);
+    }
+    return fail(ET_ERR_UNSUPPORTED, "gather row bytes %lld", (long long)rb);
+}
+
+template <typename T, typename A, bool NT>
+int launch_pooled_dim(const LookupPack& pack, int n, int D, int64_t batch, void* dst,
+                      int64_t ld_dst, hipStream_t s) {
+    switch (D) {
+        case 16: return launch_pooled_vec<T, A, 16, NT>(pack, n, batch, dst, ld_dst, s);
+        case 32: return launch_pooled_vec<T, A, 32, NT>(pack, n, batch, dst, ld_dst, s);
+        case 64: return launch_pooled_vec<T, A, 64, NT>(pack, n, batch, dst, ld_dst, s);
+        case 128: return launch_pooled_vec<T, A, 128, NT>(pack, n, batch, dst, ld_dst, s);
+        case 256: return launch_pooled_vec<T, A, 256, NT>(pack, n, batch, dst, ld_dst, s);
+        case 512: return launch_pooled_vec<T, A, 512, NT>(pack, n, batch, dst, ld_dst, s);
+    }
+    return fail(ET_ERR_UNSUPPORTED, "vector dim %d", D);
+}
+
+template <typename T, typename A, bool NT>
+int launch_generic(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
+                   hipStream_t s) {
+    const int64_t grid = (batch + 3) / 4 * n;
+    if (grid <= 0) return ET_OK;
+    if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+    hipLaunchKernelGGL((k_pooled_generic<T, A, NT>), dim3((unsigned)grid), dim3(256), 0, s, pack,
+                       n, batch, reinterpret_cast<T*>(dst), ld_dst);
+    ET_LAUNCH_CHECK("k_pooled_generic");
+    return ET_OK;
+}
+
+// Kinds of launch group.
+enum GroupKind { kGather = 0, kPooledVec = 1, kGeneric = 2 };
+
+template <typename T, typename A, bool NT>
+int launch_group_typed(GroupKind kind, const LookupPack& pack, int n, int D, int64_t batch,
+                       void* dst, int64_t ld_dst, hipStream_t s) {
+    const int es = (int)sizeof(T);
+    if (kind == kGather)
+        return launch_gather<NT>(pack, n, (int64_t)D * es, batch, dst, ld_dst, es, s);
+    if (kind == kPooledVec) return launch_pooled_dim<T, A, NT>(pack, n, D, batch, dst, ld_dst, s);
+    return launch_generic<T, A, NT>(pack, n, batch, dst, ld_dst, s);
+}
+
+template <bool NT>
+int launch_group(int dtype, bool f32acc, GroupKind kind, const LookupPack& pack, int n, int D,
+                 int64_t batch, void* dst, int64_t ld_dst, hipStream_t s) {
+    switch (dtype) {
+        case ET_F32:
+            return launch_group_typed<float, float, NT>(kind, pack, n, D, batch, dst, ld_dst, s);
+        case ET_F64:
+            return launch_group_typed<double, double, NT>(kind, pack, n, D, batch, dst, ld_dst, s);
+        case ET_I32:
+            return launch_group_typed<int32_t, uint32_t, NT>(kind, pack, n, D, batch, dst, ld_dst,
+                                                            s);
+        case ET_I64:
+            return launch_group_typed<int64_t, uint64_t, NT>(kind, pack, n, D, batch, dst, ld_dst,
+                                                            s);
+        case ET_F16:
+            if (f32acc)
+                return launch_group_typed<_Float16, float, NT>(kind, pack, n, D, batch, dst,
+                                                               ld_dst, s);
+            return launch_group_typed<_Float16, _Float16, NT>(kind, pack, n, D, batch, dst, ld_dst,
+                                                              s);
+    }
+    return fail(ET_ERR_UNSUPPORTED, "dtype %d", dtype);
+}
+
+// Validate descriptors, partition them into launch groups and launch.
+// force_gather: every table is a vector (pool == 1) lookup => bit-copy path.
+int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t batch,
+                    void* dst, int64_t ld_dst, uint32_t flags, hipStream_t s) {
+    const int es = elsize(dtype);
+    if (es == 0) return fail(ET_ERR_UNSUPPORTED, "unknown dtype %d", dtype);
+    if (ntables < 0 || batch < 0) return fail(ET_ERR_ARG, "negative ntables/batch");
+    if (ntables == 0 || batch == 0) return ET_OK;
+    if (!descs) return fail(ET_ERR_ARG, "descs is NULL");
+    if (!dst) return fail(ET_ERR_ARG, "dst is NULL");
+    for (int t = 0; t < ntables; ++t) {
+        const et_lookup_desc& d = descs[t];
+        if (d.dim < 0 || d.pool < 0 || d.nrows < 0)
+            return fail(ET_ERR_ARG, "table %d: negative dim/pool/nrows", t);
+        if (d.dim == 0) continue;
+        if (d.ld_table < d.dim) return fail(ET_ERR_ARG, "table %d: ld_table < dim", t);
+        if (d.dst_row_off < 0 || d.dst_row_off + d.dim > ld_dst)
+            return fail(ET_ERR_ARG, "table %d: rows [%lld, %lld) outside ld_dst %lld", t,
+                        (long long)d.dst_row_off, (long long)(d.dst_row_off + d.dim),
+                        (long long)ld_dst);
+        if (d.pool > 0) {
+            if (!d.table || !d.idx) return fail(ET_ERR_ARG, "table %d: NULL table/idx", t);
+            if (d.nrows == 0)
+                return fail(ET_ERR_ARG, "table %d: indices into an empty table", t);
+            if (d.ld_idx < d.pool) return fail(ET_ERR_ARG, "table %d: ld_idx < pool", t);
+        }
+    }
+    const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
+    const bool f32acc = (flags & ET_FLAG_F16_FP32_ACC) != 0;
+
+    // Classify each table; group identical (kind, dim) tables into one launch.
+    int kind_of[4096];
+    if (ntables > 4096) return fail(ET_ERR_ARG, "too many tables (%d)", ntables);
+    for (int t = 0; t < ntables; ++t) {
+        const et_lookup_desc& d = descs[t];
+        const bool al = aligned16(d.table) && ((d.ld_table * es) % 16 == 0) &&
+                        aligned16(static_cast<char*>(dst) + d.dst_row_off * es) &&
+                        ((ld_dst * es) % 16 == 0);
+        if (d.dim == 0) {
+            kind_of[t] = -1;
+        } else if (d.pool == 1 && al && gather_rb_ok((int64_t)d.dim * es)) {
+            kind_of[t] = kGather;
+        } else if (d.pool >= 1 && al && vec_dim_ok(d.dim)) {
+            kind_of[t] = kPooledVec;
+        } else {
+            kind_of[t] = kGeneric;
+        }
+    }
+    bool done[4096] = {false};
+    for (int t0 = 0; t0 < ntables; ++t0) {
+        if (done[t0] || kind_of[t0] < 0) continue;
+        // Collect the group of t0 (same kind, and same dim unless generic).
+        LookupPack pack;
+        int n = 0;
+        const GroupKind kind = (GroupKind)kind_of[t0];
+        const int D = descs[t0].dim;
+        for (int t = t0; t < ntables; ++t) {
+            if (done[t] || kind_of[t] != kind_of[t0]) continue;
+            if (kind != kGeneric && descs[t].dim != D) continue;
+            pack.d[n++] = descs[t];
+            done[t] = true;
+            if (n == ET_MAX_TABLES_PER_LAUNCH) {
+                int rc = nt ? launch_group<true>(dtype, f32acc, kind, pack, n, D, batch, dst,
+                                                 ld_dst, s)
+                            : launch_group<false>(dtype, f32acc, kind, pack, n, D, batch, dst,
+                                                  ld_dst, s);
+                if (rc != ET_OK) return rc;
+                n = 0;
+            }
+        }
+        if (n > 0) {
+            int rc = nt ? launch_group<true>(dtype, f32acc, kind, pack, n, D, batch, dst, ld_dst, s)
+                        : launch_group<false>(dtype, f32acc, kind, pack, n, D, batch, dst,
+                                              ld_dst, s);
+            if (rc != ET_OK) return rc;
+        }
+    }
+    return ET_OK;
+}
+
+}  // namespace et
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+
+extern "C" int et_gather(int dtype, const void* table, int64_t ld_table, int64_t nrows,
+                         int32_t dim, const int64_t* idx, int64_t n, void* dst, int64_t ld_dst,
+                         uint32_t flags, void* stream) {
+    et::clear_err();
+    if (dim > 0 && ld_dst < dim) return et::fail(ET_ERR_ARG, "ld_dst < dim");
+    et_lookup_desc d;
+    d.table = table;
+    d.ld_table = ld_table;
+    d.nrows = nrows;
+    d.dim = dim;
+    d.pool = 1;
+    d.idx = idx;
+    d.ld_idx = 1;
+    d.dst_row_off = 0;
+    // A non-reducing lookup is a bit copy whatever the dtype: never the fp32-acc mode.
+    return et::lookup_dispatch(dtype, &d, 1, n, dst, ld_dst, flags & ~ET_FLAG_F16_FP32_ACC,
+                               static_cast<hipStream_t>(stream));
+}
+
+extern "C" int et_pooled_sum(int dtype, const void* table, int64_t ld_table, int64_t nrows,
+                             int32_t dim, const int64_t* idx, int32_t pool, int64_t ld_idx,
+                             int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
+                             void* stream) {
+    et::clear_err();
+    if (dim > 0 && ld_dst < dim) return et::fail(ET_ERR_ARG, "ld_dst < dim");
+    // pool == 0: the sum over an empty bag is zero(T); the generic kernel writes zeros.
+    et_lookup_desc d;
+    d.table = table;
+    d.ld_table = ld_table;
+    d.nrows = nrows;
+    d.dim = dim;
+    d.pool = pool;
+    d.idx = idx;
+    d.ld_idx = ld_idx;
+    d.dst_row_off = 0;
+    // pool == 1 as a *matrix* index is still a sum of one row == that row.
+    return et::lookup_dispatch(dtype, &d, 1, batch, dst, ld_dst,
+                               pool == 1 ? (flags & ~ET_FLAG_F16_FP32_ACC) : flags,
+                               static_cast<hipStream_t>(stream));
+}
+
+extern "C" int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int32_t ntables,
+                                     int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
+                                     void* stream) {
+    et::clear_err();
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // Empty bags (pool == 0) are handled by the generic kernel, which writes zeros.
+    // f16 pool == 1 tables are bit copies; the flag only matters for pool >= 2, where the
+    // group kind is kPooledVec / kGeneric.
+    return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags, s);
+}

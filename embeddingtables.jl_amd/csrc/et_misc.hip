@@ -1,0 +1,157 @@
+// et_misc.hip — ABI housekeeping, synthetic-data fills and the multi-GPU concat
+// assembly (included by embtab.hip).
+#include "et_common.h"
+
+namespace et {
+
+// Same arithmetic as oracle/embtab_oracle.c:fill_range (fma in double, then one
+// rounding to the element type) so CPU and GPU fills are bit-identical.
+template <typename T>
+__global__ __launch_bounds__(256) void k_fill_uniform(T* __restrict__ dst, int64_t n,
+                                                      uint64_t seed, uint64_t offset, double lo,
+                                                      double span) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * 256) {
+        const uint64_t h = fill_hash(seed, offset + (uint64_t)i);
+        const double u = (double)(h >> 40) * (1.0 / 16777216.0);
+        const double v = __fma_rn(span, u, lo);
+        if constexpr (sizeof(T) == 2)
+            dst[i] = (T)(float)v;  // double -> float -> half, as the oracle does
+        else if constexpr (__is_same(T, int32_t) || __is_same(T, int64_t))
+            dst[i] = (T)floor(v);
+        else
+            dst[i] = (T)v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fill_index(int64_t* __restrict__ idx, int64_t n,
+                                                    uint64_t nrows, uint64_t seed,
+                                                    uint64_t offset) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * 256) {
+        const uint64_t h = fill_hash(seed, offset + (uint64_t)i);
+        idx[i] = 1 + (int64_t)__umul64hi(h, nrows);
+    }
+}
+
+// dst[off_r + f, j] = slab_r[f, j] for f < rows_r: one wave per (rank, bag) row segment.
+struct ConcatPack {
+    int32_t rows[64];
+    int64_t off[64];
+};
+
+__global__ __launch_bounds__(256) void k_concat_slabs(const char* __restrict__ slabs, int nranks,
+                                                      int64_t slab_ld_b, int64_t batch,
+                                                      ConcatPack pack, char* __restrict__ dst,
+                                                      int64_t ld_dst_b, int es) {
+    const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int r = (int)(w % nranks);
+    const int64_t j = w / nranks;
+    if (j >= batch) return;
+    const int64_t nb = (int64_t)pack.rows[r] * es;
+    const char* src = slabs + ((int64_t)r * batch + j) * slab_ld_b;
+    char* out = dst + j * ld_dst_b + pack.off[r] * es;
+    if (((uintptr_t)src & 15) == 0 && ((uintptr_t)out & 15) == 0 && (nb & 15) == 0) {
+        for (int64_t b = (int64_t)lane * 16; b < nb; b += 64 * 16)
+            *reinterpret_cast<u32x4*>(out + b) = *reinterpret_cast<const u32x4*>(src + b);
+    } else {
+        for (int64_t b = lane; b < nb; b += 64) out[b] = src[b];
+    }
+}
+
+}  // namespace et
+
+extern "C" int et_abi_version(void) { return ET_ABI_VERSION; }
+
+extern "C" const char* et_last_error(void) { return et::err_buf(); }
+
+extern "C" int et_fill_uniform(int dtype, void* dst, int64_t n, uint64_t seed, uint64_t offset,
+                               double lo, double hi, void* stream) {
+    et::clear_err();
+    if (n < 0) return et::fail(ET_ERR_ARG, "negative n");
+    if (n == 0) return ET_OK;
+    if (!dst) return et::fail(ET_ERR_ARG, "dst is NULL");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    const double span = hi - lo;
+    switch (dtype) {
+        case ET_F32:
+            hipLaunchKernelGGL(et::k_fill_uniform<float>, dim3(blocks), dim3(256), 0, s,
+                               (float*)dst, n, seed, offset, lo, span);
+            break;
+        case ET_F64:
+            hipLaunchKernelGGL(et::k_fill_uniform<double>, dim3(blocks), dim3(256), 0, s,
+                               (double*)dst, n, seed, offset, lo, span);
+            break;
+        case ET_F16:
+            hipLaunchKernelGGL(et::k_fill_uniform<_Float16>, dim3(blocks), dim3(256), 0, s,
+                               (_Float16*)dst, n, seed, offset, lo, span);
+            break;
+        case ET_I32:
+            hipLaunchKernelGGL(et::k_fill_uniform<int32_t>, dim3(blocks), dim3(256), 0, s,
+                               (int32_t*)dst, n, seed, offset, lo, span);
+            break;
+        case ET_I64:
+            hipLaunchKernelGGL(et::k_fill_uniform<int64_t>, dim3(blocks), dim3(256), 0, s,
+                               (int64_t*)dst, n, seed, offset, lo, span);
+            break;
+        default: return et::fail(ET_ERR_UNSUPPORTED, "dtype %d", dtype);
+    }
+    ET_LAUNCH_CHECK("k_fill_uniform");
+    return ET_OK;
+}
+
+extern "C" int et_fill_index_uniform(int64_t* idx, int64_t n, int64_t nrows, uint64_t seed,
+                                     uint64_t offset, void* stream) {
+    et::clear_err();
+    if (n < 0 || nrows <= 0) return et::fail(ET_ERR_ARG, "need n >= 0 and nrows > 0");
+    if (n == 0) return ET_OK;
+    if (!idx) return et::fail(ET_ERR_ARG, "idx is NULL");
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(et::k_fill_index, dim3(blocks), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), idx, n, (uint64_t)nrows, seed, offset);
+    ET_LAUNCH_CHECK("k_fill_index");
+    return ET_OK;
+}
+
+extern "C" int et_concat_slabs(int dtype, const void* slabs, int32_t nranks, int64_t slab_ld,
+                               int64_t batch, const int32_t* rows, const int64_t* dst_row_off,
+                               void* dst, int64_t ld_dst, void* stream) {
+    et::clear_err();
+    const int es = et::elsize(dtype);
+    if (!es) return et::fail(ET_ERR_UNSUPPORTED, "dtype %d", dtype);
+    if (nranks <= 0 || nranks > 64) return et::fail(ET_ERR_ARG, "nranks must be in 1..64");
+    if (batch <= 0) return ET_OK;
+    if (!slabs || !dst || !rows || !dst_row_off) return et::fail(ET_ERR_ARG, "NULL argument");
+    et::ConcatPack pack;
+    for (int r = 0; r < nranks; ++r) {
+        if (rows[r] < 0 || rows[r] > slab_ld) return et::fail(ET_ERR_ARG, "rank %d rows", r);
+        if (rows[r] > 0 && (dst_row_off[r] < 0 || dst_row_off[r] + rows[r] > ld_dst))
+            return et::fail(ET_ERR_ARG, "rank %d rows outside ld_dst", r);
+        pack.rows[r] = rows[r];
+        pack.off[r] = dst_row_off[r];
+    }
+    const int64_t waves = (int64_t)nranks * batch;
+    const int64_t blocks = (waves + 3) / 4;
+    if (blocks > 0x7fffffffll) return et::fail(ET_ERR_ARG, "grid too large");
+    hipLaunchKernelGGL(et::k_concat_slabs, dim3((unsigned)blocks), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), (const char*)slabs, nranks,
+                       slab_ld * es, batch, pack, (char*)dst, ld_dst * es, es);
+    ET_LAUNCH_CHECK("k_concat_slabs");
+    return ET_OK;
+}
+
+extern "C" int et_check_errors(uint64_t* oob_count) {
+    et::clear_err();
+    ET_HIP_CHECK(hipDeviceSynchronize());
+    unsigned long long v = 0, zero = 0;
+    ET_HIP_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(et::g_oob_count), sizeof(v), 0,
+                                     hipMemcpyDeviceToHost));
+    ET_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(et::g_oob_count), &zero, sizeof(zero), 0,
+                                   hipMemcpyHostToDevice));
+    if (oob_count) *oob_count = v;
+    return ET_OK;
+}

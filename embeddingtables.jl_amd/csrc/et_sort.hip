@@ -1,0 +1,256 @@
+// et_sort.hip — device-wide exclusive scan and stable LSD radix sort of
+// (uint32 key, uint32 value) pairs for gfx950 (included by embtab.hip).
+//
+// These build the GPU equivalent of the reference's Indexer (src/utils.jl:88-314):
+// sorting occurrences by table column with a STABLE sort keeps each column's
+// occurrences in occurrence order, which is the order remap! (src/utils.jl:242-272)
+// lays them out in `map`, so per-column gradient sums see the same addends in
+// the same order as the reference.
+//
+// Scan: reduce tiles -> scan tile sums (one workgroup) -> scan tiles with offset.
+// Sort pass (8-bit digit): per-tile digit histogram (LDS atomics) -> digit-major
+// exclusive scan -> stable scatter, where each tile is ranked in 16 rounds of
+// 256 keys (striped, so rounds follow input order) and each round ranks a key
+// among equal digits of lower lanes by 8 wave ballots + per-wave digit counts in LDS.
+#include "et_common.h"
+
+namespace et {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanThreads * kScanItems;  // 4096
+
+constexpr int kRsBits = 8;
+constexpr int kRsBuckets = 1 << kRsBits;
+constexpr int kRsThreads = 256;
+constexpr int kRsItems = 16;
+constexpr int kRsTile = kRsThreads * kRsItems;  // 4096
+
+inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Inclusive scan of one value per thread across a 256-thread workgroup.
+// Returns the inclusive prefix; *total receives the workgroup sum.
+__device__ __forceinline__ uint32_t block_inclusive_scan_256(uint32_t v, uint32_t* lds4,
+                                                             uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) lds4[wave] = v;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; ++w) off += lds4[w];
+    *total = lds4[0] + lds4[1] + lds4[2] + lds4[3];
+    __syncthreads();
+    return v + off;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t* __restrict__ in,
+                                                              int64_t m,
+                                                              uint32_t* __restrict__ part) {
+    __shared__ uint32_t lds4[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const int64_t i = base + r * kScanThreads + threadIdx.x;
+        if (i < m) s += in[i];
+    }
+    uint32_t total;
+    block_inclusive_scan_256(s, lds4, &total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+// Exclusive scan of part[0..np) in place by one workgroup; part[np] = total.
+__global__ __launch_bounds__(kScanThreads) void k_scan_partials(uint32_t* __restrict__ part,
+                                                                int64_t np) {
+    __shared__ uint32_t lds4[4];
+    uint32_t carry = 0;
+    for (int64_t b0 = 0; b0 < np; b0 += kScanThreads) {
+        const int64_t i = b0 + threadIdx.x;
+        const uint32_t v = i < np ? part[i] : 0u;
+        uint32_t total;
+        const uint32_t inc = block_inclusive_scan_256(v, lds4, &total);
+        if (i < np) part[i] = carry + inc - v;
+        carry += total;
+    }
+    if (threadIdx.x == 0) part[np] = carry;
+}
+
+// Blocked per-thread segments: thread t scans elements [t*16, t*16+16) of the tile.
+__global__ __launch_bounds__(kScanThreads) void k_scan_down(const uint32_t* __restrict__ in,
+                                                            uint32_t* __restrict__ out, int64_t m,
+                                                            const uint32_t* __restrict__ part) {
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t tile[kScanTile + kScanTile / 32];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    // striped, coalesced load into LDS (padded every 32 words against bank conflicts)
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const int e = r * kScanThreads + threadIdx.x;
+        const int64_t i = base + e;
+        tile[e + (e >> 5)] = i < m ? in[i] : 0u;
+    }
+    __syncthreads();
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int e = threadIdx.x * kScanItems + k;
+        v[k] = tile[e + (e >> 5)];
+        s += v[k];
+    }
+    uint32_t total;
+    const uint32_t inc = block_inclusive_scan_256(s, lds4, &total);
+    uint32_t run = part[blockIdx.x] + inc - s;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int e = threadIdx.x * kScanItems + k;
+        tile[e + (e >> 5)] = run;
+        run += v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const int e = r * kScanThreads + threadIdx.x;
+        const int64_t i = base + e;
+        if (i < m) out[i] = tile[e + (e >> 5)];
+    }
+}
+
+// Exclusive scan of m (< 2^32 total) uint32 values; out may alias in.  out[m] is NOT
+// written; the total is left in part[np].  `part` needs cdiv(m, 4096) + 1 entries.
+inline int exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t m, uint32_t* part,
+                              hipStream_t s) {
+    if (m <= 0) return ET_OK;
+    const int64_t np = cdiv64(m, kScanTile);
+    if (np > 0x7fffffffll) return fail(ET_ERR_ARG, "scan too large");
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, m, part);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, part, np);
+    hipLaunchKernelGGL(k_scan_down, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, out, m,
+                       part);
+    ET_LAUNCH_CHECK("exclusive_scan_u32");
+    return ET_OK;
+}
+
+inline int64_t scan_part_entries(int64_t m) { return cdiv64(m, kScanTile) + 1; }
+
+// --- radix sort -----------------------------------------------------------
+
+__global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restrict__ keys,
+                                                        int64_t n, int shift,
+                                                        uint32_t* __restrict__ hist,
+                                                        int64_t nblk) {
+    __shared__ uint32_t h[4][kRsBuckets];
+    const int wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 4 * kRsBuckets; i += kRsThreads) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+#pragma unroll 4
+    for (int r = 0; r < kRsItems; ++r) {
+        const int64_t i = base + r * kRsThreads + threadIdx.x;
+        if (i < n) atomicAdd(&h[wave][(keys[i] >> shift) & (kRsBuckets - 1)], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < kRsBuckets; d += kRsThreads)
+        hist[(int64_t)d * nblk + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+}
+
+__global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
+    const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
+    const uint32_t* __restrict__ hist_scanned, int64_t nblk) {
+    __shared__ uint32_t base_of[kRsBuckets];
+    __shared__ uint32_t wcnt[4][kRsBuckets];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < kRsBuckets; d += kRsThreads) {
+        base_of[d] = hist_scanned[(int64_t)d * nblk + blockIdx.x];
+        wcnt[0][d] = wcnt[1][d] = wcnt[2][d] = wcnt[3][d] = 0;
+    }
+    __syncthreads();
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    for (int r = 0; r < kRsItems; ++r) {
+        const int64_t i = base + r * kRsThreads + threadIdx.x;
+        const bool valid = i < n;
+        const uint32_t key = valid ? kin[i] : 0u;
+        const uint32_t val = valid ? vin[i] : 0u;
+        const uint32_t d = (key >> shift) & (kRsBuckets - 1);
+        // lanes of this wave holding the same digit
+        uint64_t same = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < kRsBits; ++b) {
+            const uint64_t ones = __ballot((d >> b) & 1u);
+            same &= ((d >> b) & 1u) ? ones : ~ones;
+        }
+        const uint32_t rank = __popcll(same & lt_mask);
+        if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(same);
+        __syncthreads();
+        uint32_t pos = 0;
+        if (valid) {
+            pos = base_of[d] + rank;
+            for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
+        }
+        __syncthreads();
+        for (int dd = threadIdx.x; dd < kRsBuckets; dd += kRsThreads) {
+            base_of[dd] += wcnt[0][dd] + wcnt[1][dd] + wcnt[2][dd] + wcnt[3][dd];
+            wcnt[0][dd] = wcnt[1][dd] = wcnt[2][dd] = wcnt[3][dd] = 0;
+        }
+        __syncthreads();
+        if (valid) {
+            kout[pos] = key;
+            vout[pos] = val;
+        }
+    }
+}
+
+struct SortBuffers {
+    uint32_t* ka;
+    uint32_t* va;
+    uint32_t* kb;
+    uint32_t* vb;
+    uint32_t* hist;  // kRsBuckets * nblk + 1
+    uint32_t* part;  // scan partials
+};
+
+inline int64_t sort_hist_entries(int64_t n) { return (int64_t)kRsBuckets * cdiv64(n, kRsTile) + 1; }
+
+// Stable sort of (ka, va) by the low `bits` key bits.  On return *sorted_k / *sorted_v
+// point at the buffers (a or b) holding the result.
+inline int radix_sort_pairs(SortBuffers& sb, int64_t n, int bits, uint32_t** sorted_k,
+                            uint32_t** sorted_v, hipStream_t s) {
+    uint32_t *k0 = sb.ka, *v0 = sb.va, *k1 = sb.kb, *v1 = sb.vb;
+    if (n > 0) {
+        const int64_t nblk = cdiv64(n, kRsTile);
+        if (nblk > 0x7fffffffll) return fail(ET_ERR_ARG, "sort too large");
+        for (int shift = 0; shift < bits; shift += kRsBits) {
+            hipLaunchKernelGGL(k_rs_hist, dim3((unsigned)nblk), dim3(kRsThreads), 0, s, k0, n,
+                               shift, sb.hist, nblk);
+            ET_LAUNCH_CHECK("k_rs_hist");
+            int rc = exclusive_scan_u32(sb.hist, sb.hist, (int64_t)kRsBuckets * nblk, sb.part, s);
+            if (rc != ET_OK) return rc;
+            hipLaunchKernelGGL(k_rs_scatter, dim3((unsigned)nblk), dim3(kRsThreads), 0, s, k0, v0,
+                               k1, v1, n, shift, sb.hist, nblk);
+            ET_LAUNCH_CHECK("k_rs_scatter");
+            uint32_t* t = k0;
+            k0 = k1;
+            k1 = t;
+            t = v0;
+            v0 = v1;
+            v1 = t;
+        }
+    }
+    *sorted_k = k0;
+    *sorted_v = v0;
+    return ET_OK;
+}
+
+inline int bits_for(uint64_t maxval) {
+    int b = 0;
+    while (b < 32 && (maxval >> b) != 0) ++b;
+    return b;
+}
+
+}  // namespace et

@@ -1,0 +1,851 @@
+// et_update.hip — fused sparse SGD (Flux.Descent) and the device Indexer for gfx950
+// (included by embtab.hip).
+//
+// Replaces (darchr/EmbeddingTables.jl):
+//   update!(::Descent, table, ::SparseEmbeddingUpdate, indexer, Val)  src/sparseupdate.jl:160-178
+//   index! / histogram! / prefixsum! / remap!                         src/utils.jl:131-314
+//   _update_specialized_impl! / _update_generic_impl!                 src/sparseupdate.jl:57-154
+//   multi-table update!(opt, tables, grads, indexers; num_splits)     src/sparseupdate.jl:199-238
+//
+// Pipeline (all stream-ordered, no host synchronisation):
+//   1. k_build_keys   occurrence o of table t -> key = row_off[t] + (col - 1), value = o
+//                      (o enumerates (table, bag, entry) with the entry fastest — the
+//                      reference's `columns(A)` order, src/utils.jl:69-86)
+//   2. radix sort      stable, so equal keys keep occurrence order (= remap! order)
+//   3. segments        run boundaries of equal keys -> distinct (table, column) pairs
+//   4. chunks          each segment is cut into chunks of at most kChunk occurrences
+//                      (unless ET_FLAG_EXACT_UPDATE), so a Zipf-hot column cannot
+//                      serialise one wave for milliseconds
+//   5. k_sgd_chunks    one lane group per chunk: acc = +0; acc += delta[:, bag] in
+//                      order; single-chunk segments apply the update directly,
+//                      others write a partial row
+//   6. k_sgd_combine   multi-chunk segments: acc = +0; acc += partial[p] in chunk order;
+//                      apply the update
+// The update of one column is  w = fma(-eta, acc, w)  (fused, the specialized path)
+// or  w = w - eta*acc  (unfused, the generic path; optionally evaluated in Float64 as
+// the reference's multi-table generic path does), chosen by ET_FLAG_SGD_UNFUSED /
+// ET_FLAG_SGD_F64_ALPHA.
+#include "et_common.h"
+#include "et_sort.hip"
+
+namespace et {
+
+constexpr uint32_t kChunk = 512;  // occurrences per chunk (non-exact mode)
+
+struct UpdatePack {
+    et_update_desc d[ET_MAX_TABLES_PER_LAUNCH];
+    uint32_t row_off[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of nrows
+    uint32_t occ_off[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of pool * batch
+};
+
+// Counters in the workspace.
+enum { kCntU = 0, kCntC = 1, kCntSlots = 16 };
+
+__device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, uint32_t key) {
+    int t = 0;
+    // ntables <= 32: a short scan of the (scalar-cached) prefix array
+    while (t + 1 < ntables && key >= p.row_off[t + 1]) ++t;
+    return t;
+}
+
+// 1. keys / values -----------------------------------------------------------
+__global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, int ntables,
+                                                    uint32_t* __restrict__ keys,
+                                                    uint32_t* __restrict__ vals, uint32_t sent) {
+    const uint32_t n = pack.occ_off[ntables];
+    for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < n;
+         o += (int64_t)gridDim.x * 256) {
+        int t = 0;
+        while (t + 1 < ntables && (uint32_t)o >= pack.occ_off[t + 1]) ++t;
+        const et_update_desc& d = pack.d[t];
+        const uint32_t ol = (uint32_t)o - pack.occ_off[t];
+        const uint32_t j = ol / (uint32_t)d.pool, i = ol - j * (uint32_t)d.pool;
+        const uint64_t col = (uint64_t)(d.idx[(int64_t)j * d.ld_idx + i] - 1);
+        uint32_t key = sent;
+        if (col < (uint64_t)d.nrows)
+            key = pack.row_off[t] + (uint32_t)col;
+        else
+            note_oob();
+        keys[o] = key;
+        vals[o] = (uint32_t)o;
+    }
+}
+
+// 3. segments ------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_seg_flags(const uint32_t* __restrict__ keys, int64_t n,
+                                                   uint32_t* __restrict__ flag) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+// flag (as read) / segid (exclusive scan of flag) -> seg_start, U.
+__global__ __launch_bounds__(256) void k_seg_start(const uint32_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ segid, int64_t n,
+                                                   uint32_t* __restrict__ seg_start,
+                                                   uint32_t* __restrict__ counters) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const bool head = (i == 0 || keys[i] != keys[i - 1]);
+    if (head) seg_start[segid[i]] = (uint32_t)i;
+    if (i == n - 1) {
+        const uint32_t U = segid[i] + 1u;
+        seg_start[U] = (uint32_t)n;
+        counters[kCntU] = U;
+    }
+}
+
+// nchunks per segment (0 beyond U), multi-chunk partial slots per segment.
+__global__ __launch_bounds__(256) void k_seg_chunks(const uint32_t* __restrict__ seg_start,
+                                                    int64_t n, const uint32_t* __restrict__ counters,
+                                                    uint32_t chunk, uint32_t* __restrict__ nch,
+                                                    uint32_t* __restrict__ multi) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (u > n) return;
+    const uint32_t U = counters[kCntU];
+    uint32_t c = 0;
+    if (u < U) {
+        const uint32_t len = seg_start[u + 1] - seg_start[u];
+        c = len <= chunk ? 1u : (len + chunk - 1) / chunk;
+    }
+    nch[u] = c;
+    multi[u] = c > 1 ? c : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_chunk_seg(const uint32_t* __restrict__ chunk_start,
+                                                   const uint32_t* __restrict__ counters,
+                                                   int64_t n, uint32_t* __restrict__ chunk_seg,
+                                                   uint32_t* __restrict__ counters_out) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t U = counters[kCntU];
+    if (u == 0) counters_out[kCntC] = chunk_start[U];
+    if (u >= U) return;
+    for (uint32_t c = chunk_start[u]; c < chunk_start[u + 1]; ++c) chunk_seg[c] = (uint32_t)u;
+    (void)n;
+}
+
+// 5./6. gradient sums and the update ---------------------------------------------
+
+template <int MODE>  // 0 fused fma, 1 unfused f32, 2 unfused f64 alpha
+__device__ __forceinline__ float sgd_apply(float w, float acc, float eta32, double eta64) {
+    if constexpr (MODE == 0) return __builtin_fmaf(-eta32, acc, w);
+    if constexpr (MODE == 1) return __fsub_rn(w, __fmul_rn(eta32, acc));
+    return (float)__dsub_rn((double)w, __dmul_rn(eta64, (double)acc));
+}
+
+// Sum delta columns of occurrences [s0, s1) of the sorted order into acc (one lane
+// group, feature vector of D fp32 as 16-B vectors).  Values are occurrence ids;
+// bag = (o - occ_off[t]) / pool_t.
+template <int D, int U>
+__device__ __forceinline__ void chunk_sum(const UpdatePack& p, int t,
+                                          const uint32_t* __restrict__ vals, uint32_t s0,
+                                          uint32_t s1, int sub, int gbase, float (&acc)[D / 4 / (D / 4 < 64 ? D / 4 : 64)][4]) {
+    constexpr int VPR = D / 4;
+    constexpr int LPR = VPR < 64 ? VPR : 64;
+    constexpr int NV = VPR / LPR;
+    const et_update_desc& d = p.d[t];
+    const float* delta = reinterpret_cast<const float*>(d.delta);
+    const uint64_t ldd = (uint64_t)d.ld_delta;
+    const uint32_t ooff = p.occ_off[t], pool = (uint32_t)d.pool;
+    for (uint32_t c0 = s0; c0 < s1; c0 += LPR) {
+        const int cnt = (int)(s1 - c0 < (uint32_t)LPR ? s1 - c0 : (uint32_t)LPR);
+        const uint32_t myo = vals[c0 + (uint32_t)(sub < cnt ? sub : cnt - 1)];
+        const uint32_t mybag = (myo - ooff) / pool;
+        int i0 = 0;
+        for (; i0 < cnt; i0 += U) {
+            const int m = cnt - i0 < U ? cnt - i0 : U;
+            u32x4 buf[U][NV];
+            uint64_t off[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int slot = i0 + (u < m ? u : m - 1);
+                const uint32_t bag = (uint32_t)__shfl((int)mybag, gbase + slot, 64);
+                off[u] = (uint64_t)bag * ldd;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const u32x4* src = reinterpret_cast<const u32x4*>(delta + off[u]) + sub;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) buf[u][v] = src[v * LPR];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u < m) {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        const u32x4 b = buf[u][v];
+                        acc[v][0] = acc[v][0] + __uint_as_float(b.x);
+                        acc[v][1] = acc[v][1] + __uint_as_float(b.y);
+                        acc[v][2] = acc[v][2] + __uint_as_float(b.z);
+                        acc[v][3] = acc[v][3] + __uint_as_float(b.w);
+                    }
+                }
+            }
+        }
+    }
+}
+
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_chunks(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ seg_start,
+    const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_seg,
+    const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ counters,
+    uint32_t chunk, float* __restrict__ partials, int pdim, uint32_t sent, float eta32,
+    double eta64) {
+    constexpr int VPR = D / 4;
+    constexpr int LPR = VPR < 64 ? VPR : 64;
+    constexpr int NV = VPR / LPR;
+    constexpr int GPW = 64 / LPR;
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR, sub = lane % LPR;
+    const uint32_t C = counters[kCntC];
+    const uint32_t groups = gridDim.x * 4 * GPW;
+    for (uint32_t c = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GPW + g; c < C; c += groups) {
+        const uint32_t u = chunk_seg[c];
+        const uint32_t pidx = c - chunk_start[u];
+        const uint32_t nchunks = chunk_start[u + 1] - chunk_start[u];
+        const uint32_t seg0 = seg_start[u], seg1 = seg_start[u + 1];
+        const uint32_t key = keys[seg0];
+        if (key == sent) continue;  // out-of-range indices: skipped
+        const int t = table_of_key(pack, ntables, key);
+        if (pack.d[t].dim != D) continue;  // another dim group's launch
+        const uint32_t s0 = seg0 + pidx * chunk;
+        const uint32_t s1 = s0 + chunk < seg1 ? s0 + chunk : seg1;
+        float acc[NV][4];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
+        chunk_sum<D, U>(pack, t, vals, s0, s1, sub, g * LPR, acc);
+        if (nchunks == 1) {
+            const et_update_desc& d = pack.d[t];
+            float* w = reinterpret_cast<float*>(d.table) +
+                       (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table;
+            u32x4* wp = reinterpret_cast<u32x4*>(w) + sub;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const u32x4 x = wp[v * LPR];
+                u32x4 y;
+                y.x = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.x), acc[v][0], eta32, eta64));
+                y.y = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.y), acc[v][1], eta32, eta64));
+                y.z = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.z), acc[v][2], eta32, eta64));
+                y.w = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.w), acc[v][3], eta32, eta64));
+                store16<NT>(wp + v * LPR, y);
+            }
+        } else {
+            float* pr = partials + (uint64_t)(partial_start[u] + pidx) * (uint64_t)pdim;
+            u32x4* pp = reinterpret_cast<u32x4*>(pr) + sub;
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                pp[v * LPR] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
+                                    __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
+        }
+    }
+}
+
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_combine(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
+    const uint32_t* __restrict__ counters, const float* __restrict__ partials, int pdim,
+    uint32_t sent, float eta32, double eta64) {
+    constexpr int VPR = D / 4;
+    constexpr int LPR = VPR < 64 ? VPR : 64;
+    constexpr int NV = VPR / LPR;
+    constexpr int GPW = 64 / LPR;
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPR, sub = lane % LPR;
+    const uint32_t Useg = counters[kCntU];
+    const uint32_t groups = gridDim.x * 4 * GPW;
+    for (uint32_t u = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GPW + g; u < Useg; u += groups) {
+        const uint32_t p0 = partial_start[u], p1 = partial_start[u + 1];
+        if (p1 == p0) continue;  // single-chunk segment: already applied
+        const uint32_t key = keys[seg_start[u]];
+        if (key == sent) continue;
+        const int t = table_of_key(pack, ntables, key);
+        if (pack.d[t].dim != D) continue;
+        float acc[NV][4];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
+        for (uint32_t q = p0; q < p1; ++q) {
+            const u32x4* pp = reinterpret_cast<const u32x4*>(partials + (uint64_t)q * pdim) + sub;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const u32x4 b = pp[v * LPR];
+                acc[v][0] = acc[v][0] + __uint_as_float(b.x);
+                acc[v][1] = acc[v][1] + __uint_as_float(b.y);
+                acc[v][2] = acc[v][2] + __uint_as_float(b.z);
+                acc[v][3] = acc[v][3] + __uint_as_float(b.w);
+            }
+        }
+        const et_update_desc& d = pack.d[t];
+        float* w = reinterpret_cast<float*>(d.table) +
+                   (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table;
+        u32x4* wp = reinterpret_cast<u32x4*>(w) + sub;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const u32x4 x = wp[v * LPR];
+            u32x4 y;
+            y.x = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.x), acc[v][0], eta32, eta64));
+            y.y = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.y), acc[v][1], eta32, eta64));
+            y.z = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.z), acc[v][2], eta32, eta64));
+            y.w = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.w), acc[v][3], eta32, eta64));
+            store16<NT>(wp + v * LPR, y);
+        }
+    }
+}
+
+// Generic fallback (any dim / alignment): one wave per chunk or combined segment,
+// lanes over features, scalar loads.
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_chunks_generic(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ seg_start,
+    const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_seg,
+    const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ counters,
+    uint32_t chunk, float* __restrict__ partials, int pdim, uint32_t sent, float eta32,
+    double eta64, int skip_dim) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t C = counters[kCntC];
+    const uint32_t waves = gridDim.x * 4;
+    for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < C; c += waves) {
+        const uint32_t u = chunk_seg[c];
+        const uint32_t pidx = c - chunk_start[u];
+        const uint32_t nchunks = chunk_start[u + 1] - chunk_start[u];
+        const uint32_t seg0 = seg_start[u], seg1 = seg_start[u + 1];
+        const uint32_t key = keys[seg0];
+        if (key == sent) continue;
+        const int t = table_of_key(pack, ntables, key);
+        const et_update_desc& d = pack.d[t];
+        if (d.dim == skip_dim) continue;  // handled by the vector kernel
+        const uint32_t s0 = seg0 + pidx * chunk;
+        const uint32_t s1 = s0 + chunk < seg1 ? s0 + chunk : seg1;
+        const float* delta = reinterpret_cast<const float*>(d.delta);
+        for (int f = lane; f < d.dim; f += 64) {
+            float acc = 0.0f;
+            for (uint32_t o = s0; o < s1; ++o) {
+                const uint32_t bag = (vals[o] - pack.occ_off[t]) / (uint32_t)d.pool;
+                acc = acc + delta[(uint64_t)bag * (uint64_t)d.ld_delta + f];
+            }
+            if (nchunks == 1) {
+                float* w = reinterpret_cast<float*>(d.table) +
+                           (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table + f;
+                store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+            } else {
+                partials[(uint64_t)(partial_start[u] + pidx) * pdim + f] = acc;
+            }
+        }
+    }
+}
+
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_combine_generic(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
+    const uint32_t* __restrict__ counters, const float* __restrict__ partials, int pdim,
+    uint32_t sent, float eta32, double eta64, int skip_dim) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t Useg = counters[kCntU];
+    const uint32_t waves = gridDim.x * 4;
+    for (uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6); u < Useg; u += waves) {
+        const uint32_t p0 = partial_start[u], p1 = partial_start[u + 1];
+        if (p1 == p0) continue;
+        const uint32_t key = keys[seg_start[u]];
+        if (key == sent) continue;
+        const int t = table_of_key(pack, ntables, key);
+        const et_update_desc& d = pack.d[t];
+        if (d.dim == skip_dim) continue;
+        for (int f = lane; f < d.dim; f += 64) {
+            float acc = 0.0f;
+            for (uint32_t q = p0; q < p1; ++q) acc = acc + partials[(uint64_t)q * pdim + f];
+            float* w = reinterpret_cast<float*>(d.table) +
+                       (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table + f;
+            store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Workspace
+// ---------------------------------------------------------------------------
+
+struct UpdateWs {
+    uint32_t *ka, *va, *kb, *vb, *hist, *part, *flag, *seg_start, *nch, *multi, *chunk_seg,
+        *counters;
+    float* partials;
+    int64_t bytes;
+};
+
+inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+// Lay out (or size, when base == nullptr) the update workspace for n occurrences and
+// partial rows of pdim floats.
+inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk) {
+    UpdateWs w;
+    int64_t off = 0;
+    auto take = [&](int64_t bytes) -> char* {
+        char* p = base ? base + off : nullptr;
+        off += align256(bytes);
+        return p;
+    };
+    const int64_t n1 = n + 1;
+    const int64_t hist_m = sort_hist_entries(n);
+    const int64_t scan_m = hist_m > n1 + 1 ? hist_m : n1 + 1;
+    w.ka = (uint32_t*)take(4 * n1);
+    w.va = (uint32_t*)take(4 * n1);
+    w.kb = (uint32_t*)take(4 * n1);
+    w.vb = (uint32_t*)take(4 * n1);
+    w.hist = (uint32_t*)take(4 * hist_m);
+    w.part = (uint32_t*)take(4 * scan_part_entries(scan_m));
+    w.flag = (uint32_t*)take(4 * (n1 + 1));
+    w.seg_start = (uint32_t*)take(4 * (n1 + 1));
+    w.nch = (uint32_t*)take(4 * (n1 + 1));
+    w.multi = (uint32_t*)take(4 * (n1 + 1));
+    const int64_t max_chunks = n + n / chunk + 2;
+    w.chunk_seg = (uint32_t*)take(4 * max_chunks);
+    w.counters = (uint32_t*)take(4 * kCntSlots);
+    const int64_t max_partials = 2 * (n / chunk) + 2;
+    w.partials = (float*)take(4 * max_partials * (int64_t)(pdim > 0 ? pdim : 1));
+    w.bytes = off;
+    return w;
+}
+
+// Steps 1-4 shared by et_sparse_sgd: sorted keys/values, segments and chunks.
+struct Grouped {
+    uint32_t* keys;
+    uint32_t* vals;
+};
+
+inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
+                             uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s) {
+    const int64_t blocks = cdiv64(n, 256);
+    const unsigned kb_grid = (unsigned)(blocks < 65536 ? blocks : 65536);
+    hipLaunchKernelGGL(k_build_keys, dim3(kb_grid), dim3(256), 0, s, pack, ntables, w.ka, w.va,
+                       sent);
+    ET_LAUNCH_CHECK("k_build_keys");
+    SortBuffers sb{w.ka, w.va, w.kb, w.vb, w.hist, w.part};
+    int rc = radix_sort_pairs(sb, n, bits_for(sent), &out.keys, &out.vals, s);
+    if (rc != ET_OK) return rc;
+    hipLaunchKernelGGL(k_seg_flags, dim3((unsigned)blocks), dim3(256), 0, s, out.keys, n, w.flag);
+    ET_LAUNCH_CHECK("k_seg_flags");
+    // flag -> segment id (in place)
+    rc = exclusive_scan_u32(w.flag, w.flag, n, w.part, s);
+    if (rc != ET_OK) return rc;
+    hipLaunchKernelGGL(k_seg_start, dim3((unsigned)blocks), dim3(256), 0, s, out.keys, w.flag, n,
+                       w.seg_start, w.counters);
+    ET_LAUNCH_CHECK("k_seg_start");
+    const int64_t blocks1 = cdiv64(n + 1, 256);
+    hipLaunchKernelGGL(k_seg_chunks, dim3((unsigned)blocks1), dim3(256), 0, s, w.seg_start, n,
+                       w.counters, chunk, w.nch, w.multi);
+    ET_LAUNCH_CHECK("k_seg_chunks");
+    // nch -> chunk_start, multi -> partial_start (in place, n+1 entries)
+    rc = exclusive_scan_u32(w.nch, w.nch, n + 1, w.part, s);
+    if (rc != ET_OK) return rc;
+    rc = exclusive_scan_u32(w.multi, w.multi, n + 1, w.part, s);
+    if (rc != ET_OK) return rc;
+    hipLaunchKernelGGL(k_chunk_seg, dim3((unsigned)blocks), dim3(256), 0, s, w.nch, w.counters, n,
+                       w.chunk_seg, w.counters);
+    ET_LAUNCH_CHECK("k_chunk_seg");
+    return ET_OK;
+}
+
+template <int MODE, bool NT>
+int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
+                     uint32_t chunk, int pdim, uint32_t sent, float eta32, double eta64,
+                     int vec_dim, bool any_generic, hipStream_t s) {
+    const unsigned grid = 256 * 8;
+#define ET_SGD_VEC(DD)                                                                         \
+    case DD:                                                                                   \
+        hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
+                           ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg,         \
+                           w.multi, w.counters, chunk, w.partials, pdim, sent, eta32, eta64);  \
+        hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,   \
+                           ntables, gr.keys, w.seg_start, w.multi, w.counters, w.partials,     \
+                           pdim, sent, eta32, eta64);                                          \
+        break;
+    switch (vec_dim) {
+        ET_SGD_VEC(16)
+        ET_SGD_VEC(32)
+        ET_SGD_VEC(64)
+        ET_SGD_VEC(128)
+        ET_SGD_VEC(256)
+        ET_SGD_VEC(512)
+        default: break;
+    }
+#undef ET_SGD_VEC
+    ET_LAUNCH_CHECK("k_sgd_chunks");
+    if (any_generic) {
+        hipLaunchKernelGGL((k_sgd_chunks_generic<MODE, NT>), dim3(grid), dim3(256), 0, s, pack,
+                           ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg, w.multi,
+                           w.counters, chunk, w.partials, pdim, sent, eta32, eta64, vec_dim);
+        hipLaunchKernelGGL((k_sgd_combine_generic<MODE, NT>), dim3(grid), dim3(256), 0, s, pack,
+                           ntables, gr.keys, w.seg_start, w.multi, w.counters, w.partials, pdim,
+                           sent, eta32, eta64, vec_dim);
+        ET_LAUNCH_CHECK("k_sgd_chunks_generic");
+    }
+    return ET_OK;
+}
+
+inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_out,
+                           uint64_t* rows_out, int* pdim_out) {
+    if (ntables < 0) return fail(ET_ERR_ARG, "negative ntables");
+    if (ntables > ET_MAX_TABLES_PER_LAUNCH)
+        return fail(ET_ERR_ARG, "at most %d tables per update call", ET_MAX_TABLES_PER_LAUNCH);
+    if (ntables > 0 && !descs) return fail(ET_ERR_ARG, "descs is NULL");
+    int64_t n = 0;
+    uint64_t rows = 0;
+    int pdim = 0;
+    for (int t = 0; t < ntables; ++t) {
+        const et_update_desc& d = descs[t];
+        if (d.dim < 0 || d.pool < 0 || d.nrows < 0 || d.batch < 0)
+            return fail(ET_ERR_ARG, "table %d: negative size", t);
+        if (d.pool > 0 && d.batch > 0) {
+            if (!d.table || !d.delta || !d.idx) return fail(ET_ERR_ARG, "table %d: NULL", t);
+            if (d.ld_idx < d.pool) return fail(ET_ERR_ARG, "table %d: ld_idx < pool", t);
+            if (d.ld_table < d.dim || d.ld_delta < d.dim)
+                return fail(ET_ERR_ARG, "table %d: leading dimension < dim", t);
+        }
+        n += (int64_t)d.pool * d.batch;
+        rows += (uint64_t)d.nrows;
+        if (d.dim > pdim) pdim = d.dim;
+    }
+    if (n >= 0xffffffffll) return fail(ET_ERR_ARG, "too many occurrences (%lld)", (long long)n);
+    if (rows >= 0xffffffffull) return fail(ET_ERR_ARG, "too many table columns");
+    *n_out = n;
+    *rows_out = rows;
+    *pdim_out = (pdim + 3) & ~3;
+    return ET_OK;
+}
+
+}  // namespace et
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+
+extern "C" int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntables,
+                                     int64_t* bytes) {
+    et::clear_err();
+    if (!bytes) return et::fail(ET_ERR_ARG, "bytes is NULL");
+    int64_t n;
+    uint64_t rows;
+    int pdim;
+    int rc = et::validate_update(descs, ntables, &n, &rows, &pdim);
+    if (rc != ET_OK) return rc;
+    *bytes = et::carve_update_ws(nullptr, n, pdim, et::kChunk).bytes;
+    return ET_OK;
+}
+
+extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
+                             uint32_t flags, void* workspace, int64_t ws_bytes, void* stream) {
+    et::clear_err();
+    if (dtype != ET_F32) return et::fail(ET_ERR_UNSUPPORTED, "sparse SGD supports ET_F32 only");
+    int64_t n;
+    uint64_t rows;
+    int pdim;
+    int rc = et::validate_update(descs, ntables, &n, &rows, &pdim);
+    if (rc != ET_OK) return rc;
+    if (n == 0) return ET_OK;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool exact = (flags & ET_FLAG_EXACT_UPDATE) != 0;
+    // In exact mode a chunk spans a whole segment (n occurrences at most).
+    const uint32_t chunk = exact ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff) : et::kChunk;
+    et::UpdateWs w = et::carve_update_ws(static_cast<char*>(workspace), n, pdim, et::kChunk);
+    if (!workspace || ws_bytes < w.bytes)
+        return et::fail(ET_ERR_WORKSPACE, "workspace of %lld bytes needed",
+                        (long long)w.bytes);
+
+    et::UpdatePack pack;
+    uint32_t ro = 0, oo = 0;
+    int vec_dim = -1;
+    bool any_generic = false;
+    for (int t = 0; t < ntables; ++t) {
+        const et_update_desc& d = descs[t];
+        pack.d[t] = d;
+        pack.row_off[t] = ro;
+        pack.occ_off[t] = oo;
+        ro += (uint32_t)d.nrows;
+        oo += (uint32_t)(d.pool * d.batch);
+        if (d.pool == 0 || d.batch == 0 || d.dim == 0) continue;
+        const bool al = et::aligned16(d.table) && et::aligned16(d.delta) &&
+                        (d.ld_table % 4 == 0) && (d.ld_delta % 4 == 0) && et::vec_dim_ok(d.dim);
+        if (al && (vec_dim < 0 || vec_dim == d.dim))
+            vec_dim = d.dim;
+        else
+            any_generic = true;
+    }
+    pack.row_off[ntables] = ro;
+    pack.occ_off[ntables] = oo;
+    const uint32_t sent = ro;  // key of out-of-range occurrences (sorts last)
+    if (vec_dim < 0) any_generic = true;
+    // A table of vec_dim that is misaligned must not be taken by the vector kernel: the
+    // generic kernels skip only `vec_dim`, so route such tables by disabling vec.
+    for (int t = 0; t < ntables && vec_dim > 0; ++t) {
+        const et_update_desc& d = descs[t];
+        if (d.dim != vec_dim || d.pool == 0 || d.batch == 0) continue;
+        const bool al = et::aligned16(d.table) && et::aligned16(d.delta) &&
+                        (d.ld_table % 4 == 0) && (d.ld_delta % 4 == 0);
+        if (!al) {
+            vec_dim = -1;
+            any_generic = true;
+        }
+    }
+
+    et::Grouped gr;
+    rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s);
+    if (rc != ET_OK) return rc;
+
+    const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
+    const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;
+    const float eta32 = (float)eta;
+    const double eta64 = eta;
+#define ET_SGD_CALL(M, NTV)                                                                   \
+    return et::launch_sgd_typed<M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, eta32, eta64, \
+                                        vec_dim, any_generic, s)
+    if (mode == 0) {
+        if (nt) ET_SGD_CALL(0, true);
+        ET_SGD_CALL(0, false);
+    } else if (mode == 1) {
+        if (nt) ET_SGD_CALL(1, true);
+        ET_SGD_CALL(1, false);
+    }
+    if (nt) ET_SGD_CALL(2, true);
+    ET_SGD_CALL(2, false);
+#undef ET_SGD_CALL
+}
+
+// ---------------------------------------------------------------------------
+// Device Indexer in the reference's layout (first-seen order)
+// ---------------------------------------------------------------------------
+namespace et {
+
+__global__ __launch_bounds__(256) void k_first_occ(const uint32_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ vals,
+                                                   const uint32_t* __restrict__ seg_start,
+                                                   const uint32_t* __restrict__ counters,
+                                                   int64_t n, uint32_t sent, uint32_t pad,
+                                                   uint32_t* __restrict__ fo,
+                                                   uint32_t* __restrict__ seg) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (u >= n) return;
+    const uint32_t U = counters[kCntU];
+    uint32_t f = pad;
+    if (u < U && keys[seg_start[u]] != sent) f = vals[seg_start[u]];  // stable => minimum
+    fo[u] = f;
+    seg[u] = (uint32_t)u;
+}
+
+// cnt[k] = occurrences of the k-th distinct column in first-seen order (0 beyond).
+__global__ __launch_bounds__(256) void k_count_fs(const uint32_t* __restrict__ order_fo,
+                                                  const uint32_t* __restrict__ order_seg,
+                                                  const uint32_t* __restrict__ seg_start,
+                                                  int64_t n, uint32_t pad,
+                                                  uint32_t* __restrict__ cnt) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k > n) return;
+    uint32_t c = 0;
+    if (k < n && order_fo[k] != pad) {
+        const uint32_t u = order_seg[k];
+        c = seg_start[u + 1] - seg_start[u];
+    }
+    cnt[k] = c;
+}
+
+__global__ __launch_bounds__(256) void k_write_index(
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ order_fo,
+    const uint32_t* __restrict__ order_seg, const uint32_t* __restrict__ off, int64_t n,
+    uint32_t pad, uint32_t pool, int64_t* __restrict__ cum_col, int64_t* __restrict__ cum_off,
+    int64_t* __restrict__ map, int64_t* __restrict__ nunique) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    for (int64_t k = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); k < n; k += waves) {
+        const bool valid = order_fo[k] != pad;
+        const bool last_valid = valid && (k + 1 == n || order_fo[k + 1] == pad);
+        if (k == 0 && !valid && lane == 0) {  // no valid occurrence at all
+            cum_col[0] = 0;
+            cum_off[0] = 1;
+            *nunique = 0;
+        }
+        if (!valid) continue;
+        const uint32_t u = order_seg[k];
+        const uint32_t s0 = seg_start[u], len = seg_start[u + 1] - s0;
+        if (lane == 0) {
+            cum_col[k] = (int64_t)keys[s0] + 1;
+            cum_off[k] = (int64_t)off[k] + 1;
+            if (last_valid) {
+                cum_col[k + 1] = 0;
+                cum_off[k + 1] = (int64_t)off[k] + len + 1;
+                *nunique = k + 1;
+            }
+        }
+        for (uint32_t q = lane; q < len; q += 64)
+            map[off[k] + q] = (int64_t)(vals[s0 + q] / pool) + 1;
+    }
+}
+
+struct IndexWs {
+    UpdateWs u;
+    uint32_t *fk, *fv, *fk2, *fv2, *cnt;
+    int64_t bytes;
+};
+
+inline IndexWs carve_index_ws(char* base, int64_t n) {
+    IndexWs w;
+    w.u = carve_update_ws(base, n, 0, kChunk);
+    int64_t off = w.u.bytes;
+    auto take = [&](int64_t bytes) -> char* {
+        char* p = base ? base + off : nullptr;
+        off += align256(bytes);
+        return p;
+    };
+    const int64_t n1 = n + 1;
+    w.fk = (uint32_t*)take(4 * n1);
+    w.fv = (uint32_t*)take(4 * n1);
+    w.fk2 = (uint32_t*)take(4 * n1);
+    w.fv2 = (uint32_t*)take(4 * n1);
+    w.cnt = (uint32_t*)take(4 * (n1 + 1));
+    w.bytes = off;
+    return w;
+}
+
+}  // namespace et
+
+extern "C" int et_index_workspace_size(int64_t n, int64_t* bytes) {
+    et::clear_err();
+    if (!bytes || n < 0) return et::fail(ET_ERR_ARG, "bad arguments");
+    *bytes = et::carve_index_ws(nullptr, n).bytes;
+    return ET_OK;
+}
+
+extern "C" int et_index_build(const int64_t* idx, int32_t pool, int64_t ld_idx, int64_t batch,
+                              int64_t nrows, int64_t* cumulative_col, int64_t* cumulative_off,
+                              int64_t* map, int64_t* nunique_dev, void* workspace,
+                              int64_t ws_bytes, void* stream) {
+    et::clear_err();
+    if (pool < 0 || batch < 0 || nrows < 0) return et::fail(ET_ERR_ARG, "negative size");
+    const int64_t n = (int64_t)pool * batch;
+    if (n >= 0x7fffffffll) return et::fail(ET_ERR_ARG, "too many occurrences");
+    if (nrows >= 0xffffffffll) return et::fail(ET_ERR_ARG, "too many columns");
+    if (!cumulative_col || !cumulative_off || !nunique_dev || (n > 0 && (!map || !idx)))
+        return et::fail(ET_ERR_ARG, "NULL argument");
+    if (n > 0 && ld_idx < pool) return et::fail(ET_ERR_ARG, "ld_idx < pool");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (n == 0) {
+        const int64_t term[2] = {0, 1};
+        const int64_t zero = 0;
+        ET_HIP_CHECK(hipMemcpyAsync(cumulative_col, &term[0], 8, hipMemcpyHostToDevice, s));
+        ET_HIP_CHECK(hipMemcpyAsync(cumulative_off, &term[1], 8, hipMemcpyHostToDevice, s));
+        ET_HIP_CHECK(hipMemcpyAsync(nunique_dev, &zero, 8, hipMemcpyHostToDevice, s));
+        ET_HIP_CHECK(hipStreamSynchronize(s));  // the host sources are on this stack frame
+        return ET_OK;
+    }
+    et::IndexWs w = et::carve_index_ws(static_cast<char*>(workspace), n);
+    if (!workspace || ws_bytes < w.bytes)
+        return et::fail(ET_ERR_WORKSPACE, "workspace of %lld bytes needed", (long long)w.bytes);
+
+    et::UpdatePack pack;
+    et_update_desc d{};
+    d.nrows = nrows;
+    d.dim = 0;
+    d.pool = pool;
+    d.idx = idx;
+    d.ld_idx = ld_idx;
+    d.batch = batch;
+    pack.d[0] = d;
+    pack.row_off[0] = 0;
+    pack.row_off[1] = (uint32_t)nrows;
+    pack.occ_off[0] = 0;
+    pack.occ_off[1] = (uint32_t)n;
+    const uint32_t sent = (uint32_t)nrows;
+
+    et::Grouped gr;
+    int rc = et::group_occurrences(pack, 1, n, sent, et::kChunk, w.u, gr, s);
+    if (rc != ET_OK) return rc;
+
+    const uint32_t pad = (uint32_t)n;  // > every occurrence id
+    const int64_t blocks = et::cdiv64(n, 256);
+    hipLaunchKernelGGL(et::k_first_occ, dim3((unsigned)blocks), dim3(256), 0, s, gr.keys, gr.vals,
+                       w.u.seg_start, w.u.counters, n, sent, pad, w.fk, w.fv);
+    ET_LAUNCH_CHECK("k_first_occ");
+    et::SortBuffers sb{w.fk, w.fv, w.fk2, w.fv2, w.u.hist, w.u.part};
+    uint32_t *ofo, *oseg;
+    rc = et::radix_sort_pairs(sb, n, et::bits_for(pad), &ofo, &oseg, s);
+    if (rc != ET_OK) return rc;
+    hipLaunchKernelGGL(et::k_count_fs, dim3((unsigned)et::cdiv64(n + 1, 256)), dim3(256), 0, s,
+                       ofo, oseg, w.u.seg_start, n, pad, w.cnt);
+    ET_LAUNCH_CHECK("k_count_fs");
+    rc = et::exclusive_scan_u32(w.cnt, w.cnt, n + 1, w.u.part, s);
+    if (rc != ET_OK) return rc;
+    const int64_t wb = et::cdiv64(n, 4);
+    hipLaunchKernelGGL(et::k_write_index, dim3((unsigned)(wb < 65536 ? wb : 65536)), dim3(256), 0,
+                       s, gr.keys, gr.vals, w.u.seg_start, ofo, oseg, w.cnt, n, pad,
+                       (uint32_t)pool, cumulative_col, cumulative_off, map, nunique_dev);
+    ET_LAUNCH_CHECK("k_write_index");
+    return ET_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Update from a reference-layout Indexer range (IndexerView)
+// ---------------------------------------------------------------------------
+namespace et {
+
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_update_indexed(
+    float* __restrict__ table, int64_t ld_table, int64_t nrows, int dim,
+    const float* __restrict__ delta, int64_t ld_delta, const int64_t* __restrict__ cum_col,
+    const int64_t* __restrict__ cum_off, int64_t ubegin, int64_t uend,
+    const int64_t* __restrict__ map, float eta32, double eta64) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    for (int64_t e = ubegin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < uend; e += waves) {
+        const uint64_t col = (uint64_t)(cum_col[e] - 1);
+        if (col >= (uint64_t)nrows) {
+            if (lane == 0) note_oob();
+            continue;
+        }
+        const int64_t k0 = cum_off[e] - 1, k1 = cum_off[e + 1] - 1;
+        float* w = table + col * (uint64_t)ld_table;
+        for (int f = lane; f < dim; f += 64) {
+            float acc = 0.0f;  // zero(Tiled) / zero!(scratchspace)
+            for (int64_t k = k0; k < k1; ++k)
+                acc = acc + delta[(uint64_t)(map[k] - 1) * (uint64_t)ld_delta + f];
+            store_scalar<NT>(w + f, sgd_apply<MODE>(w[f], acc, eta32, eta64));
+        }
+    }
+}
+
+}  // namespace et
+
+extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table, int64_t nrows,
+                                 int32_t dim, const void* delta, int64_t ld_delta,
+                                 const int64_t* cumulative_col, const int64_t* cumulative_off,
+                                 int64_t ubegin, int64_t uend, const int64_t* map, double eta,
+                                 uint32_t flags, void* stream) {
+    et::clear_err();
+    if (dtype != ET_F32) return et::fail(ET_ERR_UNSUPPORTED, "update supports ET_F32 only");
+    if (uend <= ubegin || dim == 0) return ET_OK;
+    if (ubegin < 0 || dim < 0 || ld_table < dim || ld_delta < dim)
+        return et::fail(ET_ERR_ARG, "bad sizes");
+    if (!table || !delta || !cumulative_col || !cumulative_off || !map)
+        return et::fail(ET_ERR_ARG, "NULL argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t nb = et::cdiv64(uend - ubegin, 4);
+    const unsigned grid = (unsigned)(nb < 8192 ? nb : 8192);
+    const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
+    const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;
+    const float eta32 = (float)eta;
+#define ET_UI(M, NTV)                                                                             \
+    hipLaunchKernelGGL((et::k_update_indexed<M, NTV>), dim3(grid), dim3(256), 0, s, (float*)table, \
+                       ld_table, nrows, dim, (const float*)delta, ld_delta, cumulative_col,       \
+                       cumulative_off, ubegin, uend, map, eta32, eta)
+    if (mode == 0) {
+        if (nt) ET_UI(0, true); else ET_UI(0, false);
+    } else if (mode == 1) {
+        if (nt) ET_UI(1, true); else ET_UI(1, false);
+    } else {
+        if (nt) ET_UI(2, true); else ET_UI(2, false);
+    }
+#undef ET_UI
+    ET_LAUNCH_CHECK("k_update_indexed");
+    return ET_OK;
+}

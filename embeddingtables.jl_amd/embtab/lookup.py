@@ -1,0 +1,236 @@
+"""lookup / lookup! / maplookup / maplookup! on the HIP engine.
+
+Mirrors src/lookup.jl (darchr/EmbeddingTables.jl):
+  destination            :19-22
+  lookup / lookup!       :35-43, vector dispatch :90-102, matrix dispatch :167-182
+  ColumnWrap / colwrap   :195-213
+  DefaultStrategy        :220-241 and its rrule :246-258
+  SimpleParallelStrategy :262-276
+  PreallocationStrategy  :284-371 and its rrule :374-389
+
+Every hot call is ONE C-ABI launch on torch's current stream; there is no CPU
+path.  Names with a trailing underscore are Julia's bang functions
+(``lookup_`` = ``lookup!``).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .tables import AbstractEmbeddingTable, ArgumentError, featuresize, example
+
+
+class AbstractExecutionStrategy:
+    pass
+
+
+class DefaultStrategy(AbstractExecutionStrategy):
+    """One lookup per table (src/lookup.jl:220-241)."""
+
+
+class SimpleParallelStrategy(AbstractExecutionStrategy):
+    """Per-table parallelism (src/lookup.jl:262-276).  On the GPU every table's lookup
+    is already a full-chip launch; the result is identical to DefaultStrategy."""
+
+
+class PreallocationStrategy(AbstractExecutionStrategy):
+    """Fused lookup + concat into one ``(prependrows + sum(D)) x B`` matrix
+    (src/lookup.jl:284-291).  ``eltype`` is the reference's type parameter ``T``
+    (``Any`` = the tables' element type)."""
+
+    def __init__(self, prependrows: int = 0, eltype: torch.dtype | None = None):
+        self.prependrows = int(prependrows)
+        self.eltype = eltype
+
+    def __repr__(self):
+        return f"PreallocationStrategy({self.prependrows})"
+
+
+class NoTangent:
+    """ChainRulesCore.NoTangent()."""
+
+    _inst = None
+
+    def __new__(cls):
+        if cls._inst is None:
+            cls._inst = super().__new__(cls)
+        return cls._inst
+
+    def __repr__(self):
+        return "NoTangent()"
+
+
+# --- argument plumbing ---------------------------------------------------------------
+
+def _check_table(A):
+    if not isinstance(A, AbstractEmbeddingTable):
+        raise TypeError(f"expected an AbstractEmbeddingTable, got {type(A).__name__}")
+    if not A.example().is_cuda:
+        raise ArgumentError("the HIP engine needs tables in device memory")
+
+
+def _check_idx(I: torch.Tensor) -> torch.Tensor:
+    if not isinstance(I, torch.Tensor):
+        raise TypeError("indices must be an int64 torch tensor")
+    if I.dtype != torch.int64:
+        raise TypeError(f"indices must be int64 (Julia Int), got {I.dtype}")
+    if not I.is_cuda:
+        raise ArgumentError("indices must be in device memory")
+    if I.dim() not in (1, 2):
+        raise ArgumentError("lookup indices are a vector or a (B, P) matrix")
+    if I.numel() > 0 and I.stride(-1) != 1:
+        raise ArgumentError("a bag's indices must be contiguous (stride(-1) == 1)")
+    return I
+
+
+def _ld(x: torch.Tensor) -> int:
+    """Leading dimension (elements between consecutive Julia columns) of a 2-D tensor."""
+    if x.dim() == 1:
+        return 1
+    return int(x.stride(0)) if x.shape[0] > 1 else max(int(x.shape[1]), 1)
+
+
+def _check_dst(dst: torch.Tensor, A, B: int):
+    if not isinstance(dst, torch.Tensor) or dst.dim() != 2:
+        raise ArgumentError("destination must be a 2-D (B, D) tensor")
+    if dst.dtype != A.dtype:
+        raise ArgumentError(f"destination eltype {dst.dtype} != table eltype {A.dtype}")
+    if dst.shape[0] != B or dst.shape[1] != featuresize(A):
+        raise ArgumentError(f"destination shape {tuple(dst.shape)} != ({B}, {featuresize(A)})")
+    if dst.numel() > 0 and dst.stride(1) != 1:
+        raise ArgumentError("destination features must be contiguous")
+
+
+def _trailing_size(I: torch.Tensor) -> int:
+    """src/lookup.jl:19: size(I, ndims(I)) — the batch (torch dim 0)."""
+    return int(I.shape[0])
+
+
+def destination(A: AbstractEmbeddingTable, I: torch.Tensor) -> torch.Tensor:
+    """src/lookup.jl:20-22: ``similar(example(A), eltype(A), featuresize(A), B)``."""
+    return torch.empty((_trailing_size(I), featuresize(A)), dtype=A.dtype, device=A.device)
+
+
+# --- lookup ---------------------------------------------------------------------------
+
+def lookup(A: AbstractEmbeddingTable, I: torch.Tensor) -> torch.Tensor:
+    """``lookup(A, I)`` (src/lookup.jl:35-40): vector index -> gather, matrix -> pooled sum."""
+    _check_table(A)
+    _check_idx(I)
+    return lookup_(destination(A, I), A, I)
+
+
+def lookup_(dst: torch.Tensor, A: AbstractEmbeddingTable, I: torch.Tensor,
+            nontemporal: bool = True) -> torch.Tensor:
+    """``lookup!(dst, A, I)``: one kernel launch; returns ``dst``.
+
+    ``nontemporal`` mirrors the reference's non-temporal stores of the static path
+    (src/lookup.jl:161)."""
+    _check_table(A)
+    _check_idx(I)
+    B = _trailing_size(I)
+    _check_dst(dst, A, B)
+    L = _lib.load()
+    D, R = A.size()
+    flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
+    if I.dim() == 1:
+        rc = L.et_gather(_lib.et_dtype(dst), A.columnpointer(1), A.ld, R, D, I.data_ptr(), B,
+                         dst.data_ptr(), _ld(dst), flags, _lib.stream_handle(dst.device))
+    else:
+        P = int(I.shape[1])
+        rc = L.et_pooled_sum(_lib.et_dtype(dst), A.columnpointer(1), A.ld, R, D, I.data_ptr(), P,
+                             _ld(I), B, dst.data_ptr(), _ld(dst), flags,
+                             _lib.stream_handle(dst.device))
+    _lib.check(rc)
+    return dst
+
+
+# --- ColumnWrap (src/lookup.jl:195-213) --------------------------------------------------
+
+def colwrap(I):
+    """Vector of index arrays -> as is; a stacked tensor -> its per-table slices.
+
+    A Julia ``B x T`` matrix / ``P x B x T`` array is a torch ``(T, B)`` / ``(T, B, P)``
+    tensor, so table ``t`` is ``I[t]``."""
+    if isinstance(I, (list, tuple)):
+        return list(I)
+    if isinstance(I, torch.Tensor):
+        if I.dim() < 2:
+            raise ArgumentError("a stacked index tensor needs a table dimension")
+        return [I[t] for t in range(I.shape[0])]
+    raise TypeError(f"unsupported index container {type(I).__name__}")
+
+
+def _batchsize(I) -> int:
+    """src/lookup.jl:296-299."""
+    return _trailing_size(colwrap(I)[0])
+
+
+# --- maplookup --------------------------------------------------------------------------
+
+def maplookup(*args, **kw):
+    """``maplookup([strategy], tables, I)`` (src/lookup.jl:221-231, :305-314)."""
+    if args and isinstance(args[0], AbstractExecutionStrategy):
+        strategy, tables, I = args
+    else:
+        strategy = DefaultStrategy()
+        tables, I = args
+    if isinstance(strategy, PreallocationStrategy):
+        tables = list(tables)
+        ncols = strategy.prependrows + sum(featuresize(t) for t in tables)
+        dtype = strategy.eltype or tables[0].dtype
+        dst = torch.empty((_batchsize(I), ncols), dtype=dtype, device=tables[0].device)
+        return maplookup_(strategy, dst, tables, I, **kw)
+    Is = colwrap(I)
+    y = [destination(A, i) for A, i in zip(tables, Is)]
+    return maplookup_(strategy, y, tables, Is, **kw)
+
+
+def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal: bool = True,
+               worksize_div: int = 8):
+    """``maplookup!(strategy, dst, tables, I)``.
+
+    Default / SimpleParallel: one launch per table.  Preallocation: ONE fused launch
+    for every table (``worksize_div`` is accepted for signature parity; the GPU grid
+    replaces the reference's 8-chunks-per-table CPU work queue)."""
+    tables = list(tables)
+    Is = colwrap(I)
+    if len(Is) != len(tables):
+        raise ArgumentError(f"{len(tables)} tables but {len(Is)} index arrays")
+    if not isinstance(strategy, PreallocationStrategy):
+        return [lookup_(y, A, i, nontemporal) for y, A, i in zip(dst, tables, Is)]
+
+    if not tables:
+        return dst
+    B = _batchsize(Is)
+    k = strategy.prependrows
+    if dst.dim() != 2 or dst.shape[0] != B:
+        raise ArgumentError(f"destination must be ({B}, prependrows + sum(D))")
+    if dst.numel() > 0 and dst.stride(1) != 1:
+        raise ArgumentError("destination features must be contiguous")
+    if k + sum(featuresize(t) for t in tables) > dst.shape[1]:
+        raise ArgumentError("destination has too few rows for prependrows + sum(D)")
+    dtype = dst.dtype
+    descs = (_lib.LookupDesc * len(tables))()
+    off = k
+    for t, (A, i) in enumerate(zip(tables, Is)):
+        _check_table(A)
+        _check_idx(i)
+        if A.dtype != dtype:
+            raise NotImplementedError(
+                f"table {t} eltype {A.dtype} != destination eltype {dtype} "
+                "(PreallocationStrategy{T} conversion is not implemented on the GPU)")
+        if _trailing_size(i) != B:
+            raise ArgumentError(f"table {t}: batch {_trailing_size(i)} != {B}")
+        D, R = A.size()
+        pool = 1 if i.dim() == 1 else int(i.shape[1])
+        descs[t] = _lib.LookupDesc(A.columnpointer(1), A.ld, R, D, pool, i.data_ptr(),
+                                   1 if i.dim() == 1 else _ld(i), off)
+        off += D
+    flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
+    _lib.check(_lib.load().et_maplookup_prealloc(
+        _lib.et_dtype(dst), ctypes.addressof(descs), len(tables), B, dst.data_ptr(), _ld(dst),
+        flags, _lib.stream_handle(dst.device)))
+    return dst

@@ -1,0 +1,212 @@
+"""Table abstraction — mirrors the reference's AbstractEmbeddingTable contract.
+
+Reference: src/EmbeddingTables.jl:44-156 (AbstractEmbeddingTable, Static/Dynamic,
+featuresize, indexing contexts, columnpointer, example, getindex/setindex!) and
+src/simple.jl:1-57 (SimpleEmbedding).
+
+Layout rule used everywhere in this package: a Julia array of size
+``(d1, ..., dk)`` (column-major) is the contiguous torch tensor of shape
+``(dk, ..., d1)``.  So a ``D x R`` table is a ``(R, D)`` tensor whose row ``r-1``
+is Julia column ``r`` (one embedding vector, feature-contiguous), a ``P x B``
+index matrix is a ``(B, P)`` tensor and a ``D x B`` output is a ``(B, D)`` tensor.
+Indices are 1-based ``int64`` as in Julia.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class ArgumentError(ValueError):
+    """Julia's ArgumentError (constructor misuse, src/simple.jl:11-26)."""
+
+
+# --- lookup types (src/EmbeddingTables.jl:60-63) -------------------------------------
+
+class AbstractLookupType:
+    pass
+
+
+class _DynamicType(AbstractLookupType):
+    def __repr__(self):
+        return "Dynamic"
+
+    def __eq__(self, other):
+        return isinstance(other, _DynamicType)
+
+    def __hash__(self):
+        return hash("Dynamic")
+
+
+Dynamic = _DynamicType()
+
+
+class Static(AbstractLookupType):
+    """``Static{N}``: feature size known up front (selects the reference's fused paths)."""
+
+    def __init__(self, N):
+        if isinstance(N, bool) or not isinstance(N, int):
+            raise ArgumentError(
+                f"Expected the type parameter for `Static{{N}}` to be an Int. "
+                f"Instead, it's a {type(N).__name__}!")
+        self.N = N
+
+    def __repr__(self):
+        return f"Static{{{self.N}}}"
+
+    def __eq__(self, other):
+        return isinstance(other, Static) and other.N == self.N
+
+    def __hash__(self):
+        return hash(("Static", self.N))
+
+
+# --- indexing contexts (src/EmbeddingTables.jl:74-77) --------------------------------
+
+class IndexingContext:
+    pass
+
+
+class NoContext(IndexingContext):
+    pass
+
+
+class Forward(IndexingContext):
+    pass
+
+
+class Update(IndexingContext):
+    pass
+
+
+# --- tables ---------------------------------------------------------------------------
+
+class AbstractEmbeddingTable:
+    """A D x R table of feature-contiguous columns on one GPU.
+
+    Subtypes provide ``size()``, ``columnpointer(col, ctx)`` and ``example()``
+    (README.md:288-307); the engine additionally needs ``ld`` (elements between
+    columns) so that a kernel can address every column from the first one.
+    """
+
+    lookup_type: AbstractLookupType = Dynamic
+
+    def size(self):
+        raise NotImplementedError
+
+    def columnpointer(self, i: int, ctx: IndexingContext | None = None) -> int:
+        raise ArgumentError(f"Please explicitly define `columnpointer` for {type(self).__name__}")
+
+    def example(self) -> torch.Tensor:
+        raise NotImplementedError
+
+    @property
+    def dtype(self):
+        return self.example().dtype
+
+    @property
+    def device(self):
+        return self.example().device
+
+    def __len__(self):
+        d, r = self.size()
+        return d * r
+
+    # AbstractArray getindex / setindex! through columnpointer
+    # (src/EmbeddingTables.jl:144-156); device memory, so through a copy.
+    def __getitem__(self, ij):
+        i, j = ij
+        d, r = self.size()
+        if not (1 <= i <= d and 1 <= j <= r):
+            raise IndexError(f"BoundsError: {ij} outside {self.size()}")
+        return self._col(j)[i - 1].item()
+
+    def __setitem__(self, ij, v):
+        i, j = ij
+        d, r = self.size()
+        if not (1 <= i <= d and 1 <= j <= r):
+            raise IndexError(f"BoundsError: {ij} outside {self.size()}")
+        self._col(j)[i - 1] = v
+
+    def _col(self, j: int) -> torch.Tensor:
+        raise NotImplementedError
+
+
+class SimpleEmbedding(AbstractEmbeddingTable):
+    """Thin wrapper over a D x R column-major matrix (src/simple.jl:2-28).
+
+    ``data`` is a CUDA tensor of shape ``(R, D)`` with unit feature stride;
+    ``lookup_type`` is ``Dynamic`` (default) or ``Static(N)`` with ``N == D``.
+    """
+
+    def __init__(self, data: torch.Tensor, lookup_type: AbstractLookupType = Dynamic):
+        if not isinstance(data, torch.Tensor) or data.dim() != 2:
+            raise ArgumentError("SimpleEmbedding expects a 2-D (ncols, featuresize) tensor")
+        if data.stride(1) != 1 and data.shape[1] > 1:
+            raise ArgumentError("features of a column must be contiguous (stride(1) == 1)")
+        if isinstance(lookup_type, Static):
+            if lookup_type.N != data.shape[1]:
+                raise ArgumentError(
+                    "Parameter `N` should match the number of rows in the passed Matrix. "
+                    f"Instead, `N = {lookup_type.N}` while `size(A,1) = {data.shape[1]}`.")
+        elif lookup_type is not Dynamic:
+            raise ArgumentError(f"unknown lookup type {lookup_type!r}")
+        self.data = data
+        self.lookup_type = lookup_type
+
+    def __repr__(self):
+        d, r = self.size()
+        return f"{d}x{r} SimpleEmbedding{{{self.lookup_type!r}, {self.data.dtype}}}"
+
+    def size(self):
+        return (int(self.data.shape[1]), int(self.data.shape[0]))
+
+    @property
+    def ld(self) -> int:
+        return int(self.data.stride(0)) if self.data.shape[0] > 1 else int(self.data.shape[1])
+
+    def columnpointer(self, i: int, ctx: IndexingContext | None = None) -> int:
+        """src/simple.jl:52-55: ``pointer(A) + (i - 1) * N * sizeof(T)`` (device address)."""
+        return self.data.data_ptr() + (i - 1) * self.ld * self.data.element_size()
+
+    def example(self) -> torch.Tensor:
+        return self.data
+
+    def _col(self, j: int) -> torch.Tensor:
+        return self.data[j - 1]
+
+    def zeros(self) -> "SimpleEmbedding":
+        """``Base.zeros(::SimpleEmbedding)`` (src/simple.jl:30-34)."""
+        return SimpleEmbedding(torch.zeros_like(self.data), self.lookup_type)
+
+    def parent(self) -> torch.Tensor:
+        return self.data
+
+
+def featuresize(x) -> int:
+    """src/EmbeddingTables.jl:71-72."""
+    if isinstance(x, AbstractEmbeddingTable):
+        return x.size()[0]
+    return int(x.shape[-1])  # a (B, D) torch output is a D x B Julia matrix
+
+
+def example(x):
+    """src/EmbeddingTables.jl:118: ``example(first(x))`` for a vector of tables."""
+    if isinstance(x, (list, tuple)):
+        return x[0].example()
+    return x.example()
+
+
+def columnpointer(x, i: int, ctx: IndexingContext | None = None) -> int:
+    if isinstance(x, AbstractEmbeddingTable):
+        return x.columnpointer(i, ctx)
+    # plain (N, D) tensor: pointer(A) + strides(A)[2] * sizeof(T) * (i - 1)
+    return x.data_ptr() + (i - 1) * x.stride(0) * x.element_size()
+
+
+def fused_update_path(table: AbstractEmbeddingTable) -> bool:
+    """Which update kernel the reference dispatches to (src/sparseupdate.jl:131-154):
+    the specialized fused `muladd` path for ``Static{N}`` tables with
+    ``N * sizeof(T) <= MAX_ACCUMULATOR_SIZE / 2 = 512`` bytes, otherwise the
+    generic scratch path (``x - alpha * y``)."""
+    lt = table.lookup_type
+    return isinstance(lt, Static) and lt.N * table.example().element_size() <= 512

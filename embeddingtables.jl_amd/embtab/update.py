@@ -1,0 +1,341 @@
+"""Sparse gradients, the Indexer and the fused Descent update on the HIP engine.
+
+Mirrors (darchr/EmbeddingTables.jl):
+  SparseEmbeddingUpdate / uncompress         src/sparseupdate.jl:6-32
+  rrule(lookup)                              src/sparseupdate.jl:35-40
+  rrule(maplookup, strategy) (+ Slicer)      src/lookup.jl:247-258, :374-389, src/utils.jl:50-63
+  update!(table, grad, indexer, alpha, Val)  src/sparseupdate.jl:436-544 (specialized/generic)
+  update!(::Descent, table, grad, ...)       src/sparseupdate.jl:160-178
+  Flux.Optimise.update!(opt, x, xbar, ...)   src/sparseupdate.jl:180-189
+  multi-table update!(opt, tables, grads, indexers; num_splits, ...)  :199-238
+  Indexer / SparseIndexer / DenseIndexer / index! / IndexerView       src/utils.jl:280-338
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .lookup import (NoTangent, PreallocationStrategy, AbstractExecutionStrategy, colwrap,
+                     lookup, maplookup, _ld, _check_idx)
+from .tables import (AbstractEmbeddingTable, AbstractLookupType, ArgumentError, Dynamic,
+                     featuresize, fused_update_path)
+
+
+class SparseEmbeddingUpdate:
+    """Lazy gradient of a lookup: ``delta`` (the output gradient, a ``(B, D)`` tensor,
+    possibly a column block of a Preallocation gradient) and the forward ``indices``
+    (src/sparseupdate.jl:6-13).  Nothing is copied."""
+
+    def __init__(self, lookup_type: AbstractLookupType, delta: torch.Tensor, indices):
+        self.lookup_type = lookup_type
+        self.delta = delta
+        self.indices = indices
+
+    def __repr__(self):
+        return (f"SparseEmbeddingUpdate{{{self.lookup_type!r}}}(delta={tuple(self.delta.shape)}, "
+                f"indices={tuple(self.indices.shape)})")
+
+
+def uncompress(x: SparseEmbeddingUpdate, dstcols: int | None = None,
+               maxindices: int | None = None) -> torch.Tensor:
+    """Densify a sparse gradient into a ``(dstcols, D)`` tensor (src/sparseupdate.jl:16-32).
+    A test helper in the reference; done with device tensor ops here."""
+    I = x.indices
+    if dstcols is None:
+        dstcols = int(I.max().item())
+    D = x.delta.shape[1]
+    dst = torch.zeros((dstcols, D), dtype=x.delta.dtype, device=x.delta.device)
+    ncols = x.delta.shape[0] if maxindices is None else min(maxindices, x.delta.shape[0])
+    cols = I[:ncols].reshape(ncols, -1) - 1
+    pool = cols.shape[1]
+    src = x.delta[:ncols].repeat_interleave(pool, dim=0)
+    dst.index_add_(0, cols.reshape(-1), src)
+    return dst
+
+
+# --- rrules -----------------------------------------------------------------------------
+
+def rrule(f, *args):
+    """``ChainRulesCore.rrule`` for ``lookup`` and ``maplookup``: returns
+    ``(y, pullback)``; the pullback returns ``SparseEmbeddingUpdate``s."""
+    if f is lookup:
+        A, I = args
+        S = A.lookup_type
+        y = lookup(A, I)
+
+        def lookup_pullback(delta):
+            return (NoTangent(), SparseEmbeddingUpdate(S, delta, I), NoTangent())
+
+        return y, lookup_pullback
+    if f is maplookup:
+        strategy, tables, I = args
+        tables = list(tables)
+        Is = colwrap(I)
+        y = maplookup(strategy, tables, I)
+        if isinstance(strategy, PreallocationStrategy):
+            # Intended Slicer semantics: table t gets rows
+            # prependrows + sum(D[<t]) .+ (1:D_t) of the gradient.
+            def maplookup_pullback(delta):
+                off = strategy.prependrows
+                grads = []
+                for A, i in zip(tables, Is):
+                    D = featuresize(A)
+                    grads.append(SparseEmbeddingUpdate(A.lookup_type, delta[:, off:off + D], i))
+                    off += D
+                return (NoTangent(), NoTangent(), grads, NoTangent())
+        else:
+            def maplookup_pullback(deltas):
+                grads = [SparseEmbeddingUpdate(A.lookup_type, d, i)
+                         for A, d, i in zip(tables, deltas, Is)]
+                return (NoTangent(), NoTangent(), grads, NoTangent())
+        return y, maplookup_pullback
+    raise NotImplementedError(f"no rrule for {f!r}")
+
+
+# --- optimiser -----------------------------------------------------------------------------
+
+class Descent:
+    """Flux.Descent(eta) — the only optimiser the reference supports."""
+
+    def __init__(self, eta: float = 0.1):
+        self.eta = float(eta)
+
+    def __repr__(self):
+        return f"Descent({self.eta})"
+
+
+# --- workspaces ------------------------------------------------------------------------------
+
+_ws_cache: dict = {}
+
+
+def _workspace(nbytes: int, device, key: str) -> torch.Tensor:
+    """A cached device byte buffer of at least ``nbytes`` (allocated outside the C call)."""
+    k = (key, str(device))
+    buf = _ws_cache.get(k)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _ws_cache[k] = buf
+    return buf
+
+
+# --- Indexer ---------------------------------------------------------------------------------
+
+class AbstractIndexer:
+    pass
+
+
+class Indexer(AbstractIndexer):
+    """The reference's Indexer (src/utils.jl:288-304), built on the device by
+    ``index_``: ``cumulative`` is a ``(U + 1, 2)`` int64 tensor of ``(col, offset)``
+    pairs in first-seen order ending with ``(0, n + 1)``; ``map`` holds the gradient
+    column (bag, 1-based) of every grouped occurrence.  The Sparse (Dict) and Dense
+    (array) flavours give identical results, so both use the same device algorithm."""
+
+    flavour = "sparse"
+
+    def __init__(self):
+        self.cumulative = None
+        self.map = None
+        self.nunique = 0
+
+    @property
+    def histogram(self):
+        return None
+
+
+class SparseIndexer(Indexer):
+    flavour = "sparse"
+
+
+class DenseIndexer(Indexer):
+    flavour = "dense"
+
+
+class IndexerView(AbstractIndexer):
+    """A contiguous range of an Indexer's distinct columns (src/utils.jl:320-333)."""
+
+    def __init__(self, I: Indexer, num_splits: int, this_split: int):
+        n = I.cumulative.shape[0]  # length(I.cumulative) = U + 1
+        split = 1 + (n - 1) // num_splits  # cdiv
+        start = (this_split - 1) * split + 1
+        stop = min(this_split * split + 1, n)
+        self.I = I
+        self.range = (start, stop)  # 1-based inclusive view of cumulative
+
+    def entries(self):
+        """0-based half-open range of cumulative entries updated through this view."""
+        start, stop = self.range
+        return start - 1, max(stop - 1, start - 1)
+
+
+def index_(indexer: Indexer, A: torch.Tensor, maxindex: int) -> Indexer:
+    """``index!(indexer, A, maxindex)`` (src/utils.jl:306-314) on the device."""
+    _check_idx(A)
+    B = int(A.shape[0])
+    P = 1 if A.dim() == 1 else int(A.shape[1])
+    n = B * P
+    dev = A.device
+    L = _lib.load()
+    nb = ctypes.c_int64(0)
+    _lib.check(L.et_index_workspace_size(n, ctypes.byref(nb)))
+    ws = _workspace(nb.value, dev, "index")
+    cum = torch.empty((2, n + 1), dtype=torch.int64, device=dev)
+    mp = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    nu = torch.empty(1, dtype=torch.int64, device=dev)
+    _lib.check(L.et_index_build(A.data_ptr(), P, P if A.dim() == 1 else _ld(A), B, int(maxindex),
+                                cum[0].data_ptr(), cum[1].data_ptr(), mp.data_ptr(),
+                                nu.data_ptr(), ws.data_ptr(), ws.numel(),
+                                _lib.stream_handle(dev)))
+    U = int(nu.item())
+    indexer.nunique = U
+    indexer.cumulative = cum[:, :U + 1].t()
+    indexer.map = mp[:n]
+    return indexer
+
+
+def gettranslations(indexer: AbstractIndexer):
+    """(cumulative, map) of an Indexer / IndexerView (src/utils.jl:281, :335-338)."""
+    if isinstance(indexer, IndexerView):
+        b, e = indexer.entries()
+        return indexer.I.cumulative[b:e + 1], indexer.I.map
+    return indexer.cumulative, indexer.map
+
+
+# --- update! ------------------------------------------------------------------------------------
+
+def _sgd_flags(fused: bool, nontemporal: bool, f64_alpha: bool = False, exact: bool = False):
+    flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
+    if not fused:
+        flags |= _lib.ET_FLAG_SGD_UNFUSED
+        if f64_alpha:
+            flags |= _lib.ET_FLAG_SGD_F64_ALPHA
+    if exact:
+        flags |= _lib.ET_FLAG_EXACT_UPDATE
+    return flags
+
+
+def _update_desc(table: AbstractEmbeddingTable, grad: SparseEmbeddingUpdate) -> _lib.UpdateDesc:
+    I = _check_idx(grad.indices)
+    delta = grad.delta
+    if table.dtype != torch.float32 or delta.dtype != torch.float32:
+        raise NotImplementedError("the fused update supports Float32 tables and gradients")
+    B = int(I.shape[0])
+    P = 1 if I.dim() == 1 else int(I.shape[1])
+    D, R = table.size()
+    if delta.dim() != 2 or delta.shape[0] != B or delta.shape[1] != D:
+        raise ArgumentError(f"gradient shape {tuple(delta.shape)} != ({B}, {D})")
+    if delta.numel() > 0 and delta.stride(1) != 1:
+        raise ArgumentError("gradient features must be contiguous")
+    return _lib.UpdateDesc(table.columnpointer(1), table.ld, R, D, P, delta.data_ptr(), _ld(delta),
+                           I.data_ptr(), 1 if I.dim() == 1 else _ld(I), B)
+
+
+def _sparse_sgd(descs, eta: float, flags: int, device):
+    L = _lib.load()
+    n = len(descs)
+    arr = (_lib.UpdateDesc * n)(*descs)
+    nb = ctypes.c_int64(0)
+    _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), n, ctypes.byref(nb)))
+    ws = _workspace(nb.value, device, "sgd")
+    _lib.check(L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(arr), n, float(eta), flags,
+                               ws.data_ptr(), ws.numel(), _lib.stream_handle(device)))
+
+
+def update_(*args, nontemporal: bool | None = None, exact: bool = False, **kw):
+    """Julia's ``update!`` (multiple dispatch on the argument types):
+
+    * ``update_(opt::Descent, table, grad, [indexer], [nontemporal])`` — single table,
+      index + fused SGD in one device pipeline (src/sparseupdate.jl:160-178);
+    * ``update_(opt::Descent, tables, grads, indexers, [nontemporal]; num_splits, nthreads,
+      scratchspaces, telemetry_cb)`` — all tables in one pipeline (:199-238);
+    * ``update_(table, grad, indexer_or_view, alpha, [nontemporal])`` — update from a
+      prebuilt Indexer / IndexerView range (:436-544).
+
+    ``exact=True`` sums every column's gradient serially (bit-identical to the
+    reference even for hot columns); the default splits occurrence lists longer than
+    512 into partial sums combined in a fixed order (deterministic)."""
+    if args and isinstance(args[0], Descent):
+        opt = args[0]
+        if isinstance(args[1], AbstractEmbeddingTable):
+            table, grad = args[1], args[2]
+            nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
+            _update_single(opt, table, grad, nt, exact)
+            return None
+        tables, grads = list(args[1]), list(args[2])
+        nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
+        _update_multi(opt, tables, grads, nt, exact, **kw)
+        return None
+    table, grad, indexer, alpha = args[:4]
+    nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
+    _update_from_indexer(table, grad, indexer, float(alpha), nt)
+    return None
+
+
+def _update_single(opt: Descent, table, grad: SparseEmbeddingUpdate, nontemporal: bool,
+                   exact: bool):
+    if grad.indices.numel() == 0:
+        return
+    d = _update_desc(table, grad)
+    fused = fused_update_path(table)
+    # convert(eltype(table), opt.eta): the fp32 kernel rounds eta to Float32 itself
+    _sparse_sgd([d], opt.eta, _sgd_flags(fused, nontemporal, False, exact), table.device)
+
+
+def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool, num_splits=4,
+                  nthreads=None, scratchspaces=None, telemetry_cb=None, indexers=None):
+    if len(tables) != len(grads):
+        raise ArgumentError("tables and grads differ in length")
+    if telemetry_cb is not None:
+        telemetry_cb()
+    # Group tables by the reference's per-table path: Static <= 512 B -> specialized
+    # (Float32 eta, fused); otherwise generic with the unconverted Float64 eta
+    # (src/sparseupdate.jl:232).
+    groups: dict = {}
+    for A, g in zip(tables, grads):
+        if g.indices.numel() == 0:
+            continue
+        groups.setdefault(fused_update_path(A), []).append(_update_desc(A, g))
+    if not groups:
+        return
+    dev = tables[0].device
+    for fused, descs in groups.items():
+        flags = _sgd_flags(fused, nontemporal, not fused, exact)
+        for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
+            _sparse_sgd(descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH], opt.eta, flags, dev)
+
+
+def _update_from_indexer(table, grad: SparseEmbeddingUpdate, indexer: AbstractIndexer,
+                         alpha: float, nontemporal: bool):
+    base = indexer.I if isinstance(indexer, IndexerView) else indexer
+    if base.cumulative is None:
+        raise ArgumentError("indexer is empty: call index_(indexer, grad.indices, maxindex)")
+    if isinstance(indexer, IndexerView):
+        b, e = indexer.entries()
+    else:
+        b, e = 0, base.nunique
+    if e <= b:
+        return
+    delta = grad.delta
+    if table.dtype != torch.float32 or delta.dtype != torch.float32:
+        raise NotImplementedError("the update supports Float32 tables and gradients")
+    D, R = table.size()
+    cum = base.cumulative  # (U+1, 2) view of the (2, n+1) buffer
+    fused = fused_update_path(table)
+    _lib.check(_lib.load().et_update_indexed(
+        _lib.ET_F32, table.columnpointer(1), table.ld, R, D, delta.data_ptr(), _ld(delta),
+        cum[:, 0].data_ptr(), cum[:, 1].data_ptr(), b, e, base.map.data_ptr(), alpha,
+        _sgd_flags(fused, nontemporal), _lib.stream_handle(table.device)))
+
+
+def optimise_update_(opt, x, xbar: SparseEmbeddingUpdate, indexer=None, nontemporal=True):
+    """``Flux.Optimise.update!(opt, x, xbar::SparseEmbeddingUpdate, ...)``
+    (src/sparseupdate.jl:180-189)."""
+    return update_(opt, x, xbar, indexer, nontemporal)
+
+
+def ensemble_update(nthreads: int):
+    """src/sparseupdate.jl:195."""
+    return [Indexer() for _ in range(nthreads)]

@@ -1,0 +1,220 @@
+/*
+ * embtab.h — C ABI of libembtab_hip.so, the MI355X (gfx950) embedding-table engine.
+ *
+ * This is the drop-in boundary for the hot path of darchr/EmbeddingTables.jl:
+ * the Julia package's `lookup!`, `maplookup!(::PreallocationStrategy, …)` and
+ * `update!(::Descent, …)` methods are re-targeted (by a thin `ccall` layer, see
+ * INTEGRATION.md) onto the entry points below.  Every entry point:
+ *
+ *   - takes plain pointers and sizes only (no torch / no Julia types);
+ *   - takes DEVICE pointers for every array argument, except arrays of
+ *     descriptors (`et_lookup_desc*`, `et_update_desc*`), which live in HOST
+ *     memory and are copied into the kernel argument segment at launch;
+ *   - is stream-ordered on the caller's `hipStream_t` (passed as `void*`;
+ *     NULL = the legacy default stream) and never synchronises the device,
+ *     allocates or frees memory, so it may be captured into a hipGraph;
+ *   - returns an `int` status (ET_OK = 0, negative = error).  The message for
+ *     the last error of the calling thread is `et_last_error()`.
+ *
+ * Memory layout (identical to the reference, column-major Julia arrays):
+ *   - a table is a D x R matrix whose column `r` (1-based) — one embedding
+ *     vector of D contiguous elements — starts at `table + (r-1)*ld_table`
+ *     (reference `columnpointer`, src/simple.jl:52-55, src/EmbeddingTables.jl:83-85);
+ *   - index arrays are Int64 and 1-BASED, as in Julia; a P x B index matrix
+ *     (pool P, batch B) stores bag j's P entries at `idx + j*ld_idx`;
+ *   - outputs / gradients are D x B column-major with leading dimension `ld`.
+ *   - all leading dimensions are in ELEMENTS, not bytes.
+ *
+ * Out-of-range indices are undefined behaviour in the reference
+ * (`@inbounds`, src/lookup.jl).  Here they never fault the GPU: a bad index
+ * contributes a zero row (lookup) or is skipped (update), and is counted in a
+ * device-side error word readable with `et_check_errors`.
+ */
+#ifndef EMBTAB_H
+#define EMBTAB_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ET_ABI_VERSION 1
+
+/* Status codes. */
+#define ET_OK 0
+#define ET_ERR_ARG (-1)         /* invalid argument (message in et_last_error) */
+#define ET_ERR_HIP (-2)         /* a HIP runtime call failed */
+#define ET_ERR_WORKSPACE (-3)   /* workspace missing or too small */
+#define ET_ERR_UNSUPPORTED (-4) /* dtype / mode not implemented */
+
+/* Element types of tables, outputs and gradients. */
+#define ET_F32 0
+#define ET_F16 1
+#define ET_F64 2
+#define ET_I32 3
+#define ET_I64 4
+
+/* Flags (bitwise OR). */
+#define ET_FLAG_NONTEMPORAL 1u   /* non-temporal stores of outputs / updated rows
+                                    (reference Val{Nontemporal}, src/sparseupdate.jl:165) */
+#define ET_FLAG_F16_FP32_ACC 2u  /* F16 pooled sums accumulate in fp32 and round once;
+                                    default F16 mode rounds to fp16 after every add like
+                                    Julia Float16 arithmetic */
+#define ET_FLAG_EXACT_UPDATE 4u  /* sparse SGD: never split a hot row's occurrence list, so
+                                    every row's gradient is summed serially in occurrence
+                                    order (bit-identical to the reference, slower on skew) */
+#define ET_FLAG_SGD_UNFUSED 8u   /* sparse SGD: w - eta*acc with two roundings, the
+                                    reference's generic path (src/sparseupdate.jl:57-95);
+                                    default is fma(-eta, acc, w), its specialized path
+                                    (src/sparseupdate.jl:97-129) */
+#define ET_FLAG_SGD_F64_ALPHA 16u /* with ET_FLAG_SGD_UNFUSED: evaluate w - eta*acc in
+                                    Float64, as the multi-table generic path does with the
+                                    unconverted opt.eta (src/sparseupdate.jl:232) */
+
+/* Tables per launch carried in the kernel-argument segment; longer lists are
+ * split into several launches by the library. */
+#define ET_MAX_TABLES_PER_LAUNCH 32
+
+/* ABI version compiled into the library (== ET_ABI_VERSION). */
+int et_abi_version(void);
+
+/* Message of the last failed call on this thread ("" if none). */
+const char* et_last_error(void);
+
+/* Non-reducing gather: dst[:, j] = table[:, idx[j]] for j in 0..n-1
+ * (bit copy for every dtype).
+ * Replaces lookup!(dst, A, I::AbstractVector) — reference src/lookup.jl:51-67
+ * (lookup_generic!), :70-87 (lookup_static! SVector) and dispatch :90-102. */
+int et_gather(int dtype, const void* table, int64_t ld_table, int64_t nrows, int32_t dim,
+              const int64_t* idx, int64_t n, void* dst, int64_t ld_dst, uint32_t flags,
+              void* stream);
+
+/* Reducing (pooled-sum) lookup: dst[:, j] = sum_{i=0..pool-1} table[:, idx[j*ld_idx + i]],
+ * accumulated sequentially in pool order starting from the first row (pool == 0
+ * writes zeros).
+ * Replaces lookup!(dst, A, I::AbstractMatrix) — reference src/lookup.jl:108-132
+ * (lookup_generic!), :134-165 (lookup_static_inner / lookup_static! TiledSIMD) and
+ * dispatch :167-182. */
+int et_pooled_sum(int dtype, const void* table, int64_t ld_table, int64_t nrows, int32_t dim,
+                  const int64_t* idx, int32_t pool, int64_t ld_idx, int64_t batch, void* dst,
+                  int64_t ld_dst, uint32_t flags, void* stream);
+
+/* One table of a fused multi-table lookup. */
+typedef struct et_lookup_desc {
+    const void* table;   /* device pointer to column 1 of the table */
+    int64_t ld_table;    /* elements between consecutive columns (>= dim) */
+    int64_t nrows;       /* number of columns R (embeddings) in the table */
+    int32_t dim;         /* feature size D */
+    int32_t pool;        /* P: indices per bag; 1 for a vector (non-reducing) index */
+    const int64_t* idx;  /* device pointer, 1-based Int64, bag j at idx + j*ld_idx */
+    int64_t ld_idx;      /* elements between consecutive bags' index lists */
+    int64_t dst_row_off; /* first row of this table's block in dst (prependrows + sum of
+                            previous tables' dims) */
+} et_lookup_desc;
+
+/* Fused lookup + concat (PreallocationStrategy):
+ * dst[desc[t].dst_row_off + (0:dim_t-1), j] = lookup(table_t, idx_t)[:, j] for every
+ * table t and bag j, written in place into the (ld_dst x batch) destination.
+ * Rows of dst not covered by any table (the prepended rows) are not touched.
+ * `descs` is a HOST array of `ntables` descriptors.
+ * Replaces maplookup!(::PreallocationStrategy, dst, tables, I) — reference
+ * src/lookup.jl:316-371 (and maplookup :305-314 once dst is allocated). */
+int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int32_t ntables,
+                          int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
+                          void* stream);
+
+/* One table of a (multi-table) fused sparse-SGD update. */
+typedef struct et_update_desc {
+    void* table;         /* device pointer, updated in place */
+    int64_t ld_table;
+    int64_t nrows;
+    int32_t dim;
+    int32_t pool;        /* indices per bag (1 for a vector index) */
+    const void* delta;   /* gradient wrt the lookup output: dim x batch, column j at
+                            delta + j*ld_delta (may be a row block of a Preallocation
+                            gradient, ld_delta = prependrows + sum(dims)) */
+    int64_t ld_delta;
+    const int64_t* idx;  /* the indices of the forward lookup (1-based) */
+    int64_t ld_idx;
+    int64_t batch;
+} et_update_desc;
+
+/* Bytes of device workspace needed by et_sparse_sgd for these descriptors. */
+int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntables, int64_t* bytes);
+
+/* Fused sparse SGD (Flux.Descent) over one or many tables:
+ *   for every table t and every distinct column r referenced by idx_t:
+ *     acc = +0 ; for each occurrence (in occurrence order) of r, in bag j: acc += delta_t[:, j]
+ *     table_t[:, r] = muladd(-eta, acc, table_t[:, r])   (default: fused, Float32(eta))
+ *                   = table_t[:, r] - eta*acc            (ET_FLAG_SGD_UNFUSED)
+ * Only ET_F32 tables are supported.  Without ET_FLAG_EXACT_UPDATE, occurrence lists
+ * longer than the library's chunk length are summed as per-chunk partial sums
+ * combined in chunk order (deterministic, not bit-identical to the serial sum).
+ * Replaces update!(::Descent, table, ::SparseEmbeddingUpdate, indexer, Val(NT)) —
+ * reference src/sparseupdate.jl:160-178 with index! (src/utils.jl:306-314) and
+ * _update_specialized_impl! / _update_generic_impl! (:57-154); for ntables > 1 the
+ * multi-table update!(opt, tables, grads, indexers; num_splits) :199-238. */
+int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
+                  uint32_t flags, void* workspace, int64_t ws_bytes, void* stream);
+
+/* Update from a prebuilt Indexer (et_index_build layout) over its cumulative entries
+ * [ubegin, uend) — the reference's lower-level
+ * update!(table, ::SparseEmbeddingUpdate, indexer::AbstractIndexer, alpha, Val(NT)),
+ * src/sparseupdate.jl:436-544, where an IndexerView (src/utils.jl:320-338) selects a
+ * range of distinct columns.  Every column's gradient is summed serially in `map`
+ * order (exact).  `cumulative_*` and `map` are device arrays as written by
+ * et_index_build; `eta` is the value the reference passes as `alpha`. */
+int et_update_indexed(int dtype, void* table, int64_t ld_table, int64_t nrows, int32_t dim,
+                      const void* delta, int64_t ld_delta, const int64_t* cumulative_col,
+                      const int64_t* cumulative_off, int64_t ubegin, int64_t uend,
+                      const int64_t* map, double eta, uint32_t flags, void* stream);
+
+/* Bytes of device workspace needed by et_index_build for n occurrences. */
+int et_index_workspace_size(int64_t n, int64_t* bytes);
+
+/* The reference's Indexer on the device: groups the occurrences of a P x B (or
+ * vector, pool = 1) index array by column, with the distinct columns in
+ * FIRST-SEEN order and each column's occurrences in occurrence order.
+ * Outputs (device, int64, 1-based like the reference):
+ *   cumulative_col[u], cumulative_off[u] for u < U, and the terminator
+ *   cumulative_col[U] = 0, cumulative_off[U] = n + 1;
+ *   map[k] = gradient column (bag, 1-based) of the k-th grouped occurrence;
+ *   *nunique_dev = U.
+ * Arrays must hold n+1 (cumulative) and n (map) entries.
+ * Replaces index!(::Indexer, A, maxindex) — reference src/utils.jl:306-314 with
+ * histogram! :131-167, prefixsum! :170-239, remap! :242-272. */
+int et_index_build(const int64_t* idx, int32_t pool, int64_t ld_idx, int64_t batch,
+                   int64_t nrows, int64_t* cumulative_col, int64_t* cumulative_off,
+                   int64_t* map, int64_t* nunique_dev, void* workspace, int64_t ws_bytes,
+                   void* stream);
+
+/* Assemble the Preallocation concat from per-rank slabs after an all-gather
+ * (table-wise sharding across GPUs, no counterpart in the single-process
+ * reference): slab r is a (slab_ld x batch) column-major block at
+ * slabs + r*slab_ld*batch whose first rows[r] rows are copied to
+ * dst[dst_row_off[r] + (0:rows[r]-1), :].  `rows`, `dst_row_off` are HOST arrays
+ * of nranks entries; the rank whose slab already sits in dst can be skipped by
+ * giving it rows[r] = 0. */
+int et_concat_slabs(int dtype, const void* slabs, int32_t nranks, int64_t slab_ld,
+                    int64_t batch, const int32_t* rows, const int64_t* dst_row_off, void* dst,
+                    int64_t ld_dst, void* stream);
+
+/* Deterministic synthetic data (the same counter-based hash as oracle/):
+ * element i of dst = lo + (hi-lo) * u(seed, offset + i), u in [0,1) with 24 bits. */
+int et_fill_uniform(int dtype, void* dst, int64_t n, uint64_t seed, uint64_t offset,
+                    double lo, double hi, void* stream);
+
+/* Uniform 1-based indices in 1..nrows (hash of seed, offset + i). */
+int et_fill_index_uniform(int64_t* idx, int64_t n, int64_t nrows, uint64_t seed,
+                          uint64_t offset, void* stream);
+
+/* Synchronise the device, return (and clear) the number of out-of-range indices
+ * seen by any kernel since the last call. */
+int et_check_errors(uint64_t* oob_count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EMBTAB_H */

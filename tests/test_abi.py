@@ -1,0 +1,95 @@
+"""The C-ABI library loads, exports exactly what include/embtab.h declares, its
+struct layouts match the ctypes mirrors, and argument errors come back as status
+codes — all without touching a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "embtab.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(et_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from embtab import _lib
+
+    L = _lib.load()
+    decl = declared_functions()
+    assert decl, "no declarations parsed"
+    assert sorted(_lib.EXPORTS) == decl
+    for name in decl:
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (et_\w+)", out))
+    assert set(decl) <= exported
+
+
+def test_abi_version_and_last_error():
+    from embtab import _lib
+
+    L = _lib.load()
+    assert L.et_abi_version() == _lib.ET_ABI_VERSION == 1
+    assert isinstance(L.et_last_error(), bytes)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    from embtab import _lib
+
+    prog = tmp_path / "layout.c"
+    prog.write_text(r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "embtab.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\n", sizeof(et_lookup_desc), offsetof(et_lookup_desc, dim),
+         offsetof(et_lookup_desc, idx), offsetof(et_lookup_desc, dst_row_off),
+         sizeof(et_update_desc));
+  printf("%zu %zu %zu\n", offsetof(et_update_desc, delta), offsetof(et_update_desc, idx),
+         offsetof(et_update_desc, batch));
+  return 0;
+}
+''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(prog), "-o", str(exe)],
+                   check=True)
+    l1, l2 = subprocess.run([str(exe)], capture_output=True, text=True,
+                            check=True).stdout.split("\n")[:2]
+    L, U = _lib.LookupDesc, _lib.UpdateDesc
+    assert list(map(int, l1.split())) == [ctypes.sizeof(L), L.dim.offset, L.idx.offset,
+                                          L.dst_row_off.offset, ctypes.sizeof(U)]
+    assert list(map(int, l2.split())) == [U.delta.offset, U.idx.offset, U.batch.offset]
+
+
+def test_argument_errors_need_no_gpu():
+    from embtab import _lib
+
+    L = _lib.load()
+    # ld_dst < dim is rejected before any device work
+    rc = L.et_gather(_lib.ET_F32, None, 16, 10, 16, None, 5, None, 8, 0, None)
+    assert rc == -1 and b"ld_dst" in L.et_last_error()
+    # unknown dtype
+    rc = L.et_pooled_sum(99, None, 16, 10, 16, None, 2, 2, 5, None, 16, 0, None)
+    assert rc == -4
+    # empty work is a no-op success
+    assert L.et_gather(_lib.ET_F32, None, 16, 10, 16, None, 0, None, 16, 0, None) == 0
+    # update supports F32 only
+    assert L.et_sparse_sgd(_lib.ET_F16, None, 0, 0.1, 0, None, 0, None) == -4
+    # workspace sizing is host-only arithmetic
+    d = (_lib.UpdateDesc * 1)()
+    d[0] = _lib.UpdateDesc(1 << 20, 128, 1000, 128, 20, 1 << 20, 128, 1 << 20, 20, 4096)
+    nb = ctypes.c_int64(0)
+    assert L.et_sgd_workspace_size(ctypes.addressof(d), 1, ctypes.byref(nb)) == 0
+    assert nb.value > 20 * 4096 * 16
+    assert L.et_index_workspace_size(1000, ctypes.byref(nb)) == 0 and nb.value > 0
+    # too many tables for one update call
+    big = (_lib.UpdateDesc * 33)()
+    assert L.et_sgd_workspace_size(ctypes.addressof(big), 33, ctypes.byref(nb)) == -1

@@ -1,0 +1,222 @@
+"""Parity of the HIP forward path with the oracle (bit-exact), through the C ABI.
+
+Mirrors test/lookup.jl (dims 32..1504, permutations / repeats, 12 lookups per
+output), test/map.jl (strategy equivalence over every index container) and the
+README KATs, plus the engine's own edge cases (dtypes, strided destinations,
+empty inputs, out-of-range indices)."""
+import numpy as np
+import pytest
+import torch
+
+import embtab as et
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+
+
+def host(x):
+    return x.cpu().numpy()
+
+
+def table(h, static=True):
+    return et.SimpleEmbedding(dev(h), et.Static(h.shape[1]) if static else et.Dynamic)
+
+
+def bits_equal(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def test_readme_kats(kat):
+    k = kat["readme_lookup"]
+    A = table(np.asarray(k["table_columns"], np.int64), static=False)
+    got = et.lookup(A, dev(np.array(k["vector_indices"])))
+    assert host(got).tolist() == k["vector_expected_columns"]
+    got = et.lookup(A, dev(np.array(k["matrix_indices_bags"])))
+    assert host(got).tolist() == k["matrix_expected_columns"]
+    m = kat["readme_maplookup"]
+    tabs = [table(np.asarray(m["A_columns"], np.int64), False),
+            table(np.asarray(m["B_columns"], np.int64), False)]
+    idx = [dev(np.array(m["iA"])), dev(np.array(m["iB"]))]
+    res = et.maplookup(tabs, idx)
+    assert host(res[0]).tolist() == m["expected_A_columns"]
+    assert host(res[1]).tolist() == m["expected_B_columns"]
+    comb = torch.stack(idx)  # Julia hcat(iA, iB): 3 x 2 -> torch (2, 3)
+    res2 = et.maplookup(tabs, comb)
+    assert all(torch.equal(a, b) for a, b in zip(res, res2))
+    cat = et.maplookup(et.PreallocationStrategy(), tabs, idx)
+    assert torch.equal(cat, torch.cat(res, 1))
+
+
+DIMS = [16, 32, 64, 128, 256, 512, 1024, 1504]
+
+
+@pytest.mark.parametrize("dim", DIMS)
+@pytest.mark.parametrize("static", [True, False])
+def test_lookup_parity(oracle, dim, static):
+    rng = np.random.default_rng(dim)
+    ncols = 1000
+    h = rng.random((ncols, dim), dtype=np.float32)
+    A = table(h, static)
+    for I in (rng.permutation(ncols) + 1, rng.integers(1, ncols + 1, ncols)):
+        assert bits_equal(host(et.lookup(A, dev(I))), oracle.lookup(h, I))
+    for I in (np.stack([rng.permutation(np.arange(2, ncols + 1)) for _ in range(12)], 1),
+              rng.integers(1, ncols + 1, (ncols, 12)),
+              rng.integers(1, ncols + 1, (333, 20)),
+              rng.integers(1, ncols + 1, (77, 45))):  # pool > 32: several index chunks
+        assert bits_equal(host(et.lookup(A, dev(I))), oracle.lookup(h, I))
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.int32, np.int64, np.float16])
+@pytest.mark.parametrize("dim", [16, 128, 40])
+def test_lookup_dtypes(oracle, dtype, dim):
+    rng = np.random.default_rng(1)
+    h = (rng.standard_normal((500, dim)) * 100).astype(dtype)
+    A = table(h)
+    I = rng.integers(1, 501, (200, 20))
+    assert bits_equal(host(et.lookup(A, dev(I))), oracle.pooled_sum(h, I))
+    v = rng.integers(1, 501, 300)
+    assert bits_equal(host(et.lookup(A, dev(v))), oracle.gather(h, v))
+
+
+@pytest.mark.parametrize("dim", [16, 128, 24])
+def test_f16_fp32_accumulate_mode(oracle, dim):
+    from embtab import _lib
+
+    rng = np.random.default_rng(2)
+    h = rng.standard_normal((400, dim)).astype(np.float16)
+    I = rng.integers(1, 401, (150, 20))
+    out = torch.empty((150, dim), dtype=torch.float16, device=DEV)
+    A = table(h)
+    _lib.check(_lib.load().et_pooled_sum(
+        _lib.ET_F16, A.columnpointer(1), A.ld, 400, dim, dev(I).data_ptr(), 20, 20, 150,
+        out.data_ptr(), dim, _lib.ET_FLAG_F16_FP32_ACC, _lib.stream_handle()))
+    assert bits_equal(host(out), oracle.pooled_sum(h, I, f16_fp32_acc=True))
+
+
+def test_strided_destination_and_table(oracle):
+    """lookup! into a column block of a wider matrix and from a padded table (ld > D)."""
+    rng = np.random.default_rng(3)
+    big = rng.random((300, 160), dtype=np.float32)
+    h = big[:, :128]  # ld 160
+    A = et.SimpleEmbedding(dev(big)[:, :128], et.Static(128))
+    I = rng.integers(1, 301, (64, 20))
+    dst = torch.zeros((64, 200), dtype=torch.float32, device=DEV)
+    et.lookup_(dst[:, 36:164], A, dev(I))
+    got = host(dst)
+    assert bits_equal(got[:, 36:164], oracle.pooled_sum(np.ascontiguousarray(h), I))
+    assert not got[:, :36].any() and not got[:, 164:].any()
+
+
+def test_empty_and_pool_zero():
+    A = table(np.ones((10, 128), np.float32))
+    assert et.lookup(A, torch.zeros(0, dtype=torch.int64, device=DEV)).shape == (0, 128)
+    out = et.lookup(A, torch.zeros((7, 0), dtype=torch.int64, device=DEV))
+    assert out.shape == (7, 128) and not out.any()
+
+
+def test_out_of_range_indices_are_counted_not_faulted():
+    et.check_errors()
+    A = table(np.ones((10, 128), np.float32))
+    I = torch.tensor([[1, 11], [0, 3], [2, -5]], dtype=torch.int64, device=DEV)
+    out = host(et.lookup(A, I))
+    assert et.check_errors() == 3
+    assert out[0].tolist() == [1.0] * 128  # bad rows contribute zero
+    assert et.check_errors() == 0
+
+
+@pytest.mark.parametrize("dim", [16, 64, 512])
+def test_maplookup_strategies(oracle, dim):
+    """test/map.jl:32-103 — every strategy equals reduce(vcat, map(lookup, ...)) for
+    vector-of-vectors, matrix, vector-of-matrices and 3-D index containers."""
+    rng = np.random.default_rng(dim)
+    ntables, ncols, B, P = 10, 100, 64, 10
+    hs = [rng.standard_normal((ncols, dim)).astype(np.float32) for _ in range(ntables)]
+    tabs = [table(h) for h in hs]
+    for shape in ((B,), (B, P)):
+        hidx = [rng.integers(1, ncols + 1, shape) for _ in range(ntables)]
+        ref = np.concatenate([oracle.lookup(h, i) for h, i in zip(hs, hidx)], 1)
+        vec = [dev(i) for i in hidx]
+        stacked = dev(np.stack(hidx))  # Julia B x T / P x B x T
+        for I in (vec, stacked):
+            for s in (et.DefaultStrategy(), et.SimpleParallelStrategy()):
+                assert bits_equal(np.concatenate([host(o) for o in et.maplookup(s, tabs, I)], 1),
+                                  ref)
+            assert bits_equal(host(et.maplookup(et.PreallocationStrategy(), tabs, I)), ref)
+            got = host(et.maplookup(et.PreallocationStrategy(20), tabs, I))
+            assert bits_equal(got[:, 20:], ref)
+
+
+def test_prealloc_mixed_dims_and_pools(oracle):
+    """Tables with different dims (vector + generic kernels in one call) and pools."""
+    rng = np.random.default_rng(9)
+    dims = [128, 5, 128, 64, 37, 128]
+    pools = [20, 3, 1, 20, 7, 0]
+    hs = [rng.random((50 + 10 * t, d), dtype=np.float32) for t, d in enumerate(dims)]
+    B = 100
+    hidx = [rng.integers(1, h.shape[0] + 1, (B, p)) for h, p in zip(hs, pools)]
+    got = host(et.maplookup(et.PreallocationStrategy(3), [table(h) for h in hs],
+                            [dev(i) for i in hidx]))
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=3)
+    assert bits_equal(got[:, 3:], ref[:, 3:])
+
+
+def test_many_tables_split_launches(oracle):
+    """More tables than fit one kernel-argument pack (32)."""
+    rng = np.random.default_rng(4)
+    hs = [rng.random((20, 16), dtype=np.float32) for _ in range(40)]
+    hidx = [rng.integers(1, 21, (33, 4)) for _ in hs]
+    got = host(et.maplookup(et.PreallocationStrategy(), [table(h) for h in hs],
+                            [dev(i) for i in hidx]))
+    assert bits_equal(got, oracle.maplookup_prealloc(hs, hidx))
+
+
+def test_criteo_shaped_sample(oracle):
+    """Config-3 shape (26 tables x 128, pool 20) at a small batch, with tables of the
+    small Criteo cardinalities so the oracle check is exact and fast."""
+    rng = np.random.default_rng(26)
+    card = [1460, 583, 305, 24, 12517, 633, 3, 5683, 3194, 27, 14992, 10, 5652, 2173, 4,
+            18, 15, 105, 1460, 583, 305, 24, 633, 3, 27, 10]
+    hs = [rng.random((r, 128), dtype=np.float32) for r in card]
+    hidx = [rng.integers(1, r + 1, (1000, 20)) for r in card]
+    got = host(et.maplookup(et.PreallocationStrategy(), [table(h) for h in hs],
+                            [dev(i) for i in hidx]))
+    assert bits_equal(got, oracle.maplookup_prealloc(hs, hidx, nthreads=8))
+
+
+def test_fill_matches_oracle(oracle):
+    from embtab import _lib
+
+    L = _lib.load()
+    for dtype, tdt in ((np.float32, torch.float32), (np.float16, torch.float16),
+                       (np.float64, torch.float64)):
+        x = torch.empty(100000, dtype=tdt, device=DEV)
+        _lib.check(L.et_fill_uniform(_lib.et_dtype(x), x.data_ptr(), x.numel(), 7, 123, -1.0,
+                                     1.0, _lib.stream_handle()))
+        ref = oracle.fill_uniform((100000,), dtype, 7, 123, -1.0, 1.0)
+        assert bits_equal(host(x), ref)
+    i = torch.empty(100000, dtype=torch.int64, device=DEV)
+    _lib.check(L.et_fill_index_uniform(i.data_ptr(), i.numel(), 10131227, 9, 0,
+                                       _lib.stream_handle()))
+    assert bits_equal(host(i), oracle.fill_index_uniform((100000,), 10131227, 9))
+
+
+def test_concat_slabs():
+    from embtab import _lib
+
+    rng = np.random.default_rng(6)
+    B, nranks, slab_ld = 50, 3, 12
+    slabs = rng.random((nranks, B, slab_ld), dtype=np.float32)
+    rows = np.array([12, 8, 4], np.int32)
+    offs = np.array([2, 14, 22], np.int64)
+    dst = torch.zeros((B, 26), dtype=torch.float32, device=DEV)
+    _lib.check(_lib.load().et_concat_slabs(
+        _lib.ET_F32, dev(slabs).data_ptr(), nranks, slab_ld, B, rows.ctypes.data,
+        offs.ctypes.data, dst.data_ptr(), 26, _lib.stream_handle()))
+    got = host(dst)
+    for r in range(nranks):
+        assert np.array_equal(got[:, offs[r]:offs[r] + rows[r]], slabs[r][:, :rows[r]])

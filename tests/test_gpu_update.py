@@ -1,0 +1,205 @@
+"""Parity of the HIP sparse-SGD path and device Indexer with the oracle.
+
+Mirrors test/update.jl (pullback structure, Descent update vs the dense update,
+partition exactness), test/map.jl:117-177 (gradients through maplookup and
+PreallocationStrategy) and test/misc.jl:74-110 (Indexer KAT)."""
+import numpy as np
+import pytest
+import torch
+
+import embtab as et
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV)
+
+
+def host(x):
+    return x.cpu().numpy()
+
+
+def bits_equal(a, b):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    return a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def test_indexer_kat_on_device(kat):
+    k = kat["misc_indexer"]
+    A = dev(np.array(k["A"]))
+    for ix in (et.SparseIndexer(), et.DenseIndexer()):
+        for _ in range(2):
+            et.index_(ix, A, int(max(k["A"])))
+            assert host(ix.cumulative).tolist() == k["expected_cumulative"]
+            assert host(ix.map).tolist() == k["expected_map"]
+
+
+@pytest.mark.parametrize("shape", [(1000,), (300, 20), (64, 1)])
+def test_indexer_random_vs_oracle(oracle, shape):
+    rng = np.random.default_rng(sum(shape))
+    I = rng.integers(1, 200, shape)
+    cum, mp = oracle.index_build(I, 199)
+    ix = et.index_(et.Indexer(), dev(I), 199)
+    assert bits_equal(host(ix.cumulative), cum)
+    assert bits_equal(host(ix.map), mp)
+
+
+def test_readme_update_kat(kat):
+    k = kat["readme_update"]
+    A = et.SimpleEmbedding(torch.zeros((4, 4), dtype=torch.float32, device=DEV))
+    y, back = et.rrule(et.lookup, A, dev(np.array(k["indices"])))
+    assert not host(y).any()
+    delta = dev(np.asarray(k["delta_columns"], np.float32))
+    g = back(delta)
+    assert g[0] is et.NoTangent() and g[2] is et.NoTangent()
+    assert isinstance(g[1], et.SparseEmbeddingUpdate)
+    et.update_(et.Descent(k["eta"]), A, g[1])
+    assert np.allclose(host(A.data), np.asarray(k["expected_columns_as_printed"], np.float32),
+                       rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("dim", [64, 80, 128, 256])
+@pytest.mark.parametrize("static", [True, False])
+@pytest.mark.parametrize("reducing", [False, True])
+def test_update_exact_vs_oracle(oracle, dim, static, reducing):
+    """Single-table Descent update: bit-identical to the oracle in both the fused
+    (Static <= 512 B) and unfused (generic) forms; isapprox to the dense update."""
+    rng = np.random.default_rng(dim * 2 + static)
+    ncols = 100
+    base = rng.standard_normal((ncols, dim)).astype(np.float32)
+    I = rng.integers(1, ncols + 1, (ncols, 10) if reducing else (ncols,))
+    delta = rng.standard_normal((ncols, dim)).astype(np.float32)
+    A = et.SimpleEmbedding(dev(base), et.Static(dim) if static else et.Dynamic)
+    from embtab.tables import fused_update_path
+
+    g = et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), dev(I))
+    et.update_(et.Descent(10.0), A, g)
+    ref = base.copy()
+    oracle.sgd(ref, delta, I, 10.0, fused=fused_update_path(A))
+    assert bits_equal(host(A.data), ref)
+    # uncompress vs a dense scatter (test/update.jl:294-295)
+    dense = host(et.uncompress(g, ncols))
+    acc = np.zeros((ncols, dim), np.float64)
+    Ib = I.reshape(ncols, -1)
+    for j in range(ncols):
+        for c in Ib[j]:
+            acc[c - 1] += delta[j]
+    assert np.allclose(dense, acc, rtol=3.45e-4, atol=1e-4)
+
+
+def test_update_hot_rows_chunked_vs_exact(oracle):
+    """Zipf-skewed indices: occurrence lists longer than the 512-entry chunk are summed
+    as ordered partial sums (deterministic) — within 1e-6 rel of the serial sum; the
+    exact mode is bit-identical."""
+    rng = np.random.default_rng(12)
+    ncols, dim, B, P = 5000, 128, 4096, 20
+    base = rng.standard_normal((ncols, dim)).astype(np.float32)
+    z = np.minimum(rng.zipf(1.05, (B, P)), ncols)
+    perm = rng.permutation(ncols) + 1
+    I = perm[z - 1]
+    delta = rng.standard_normal((B, dim)).astype(np.float32)
+    ref = base.copy()
+    oracle.sgd(ref, delta, I, 0.1, fused=True)
+    counts = np.bincount(I.ravel(), minlength=ncols + 1)
+    assert counts.max() > 4 * 512  # the test really has split rows
+    res = {}
+    for exact in (True, False):
+        A = et.SimpleEmbedding(dev(base), et.Static(dim))
+        et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta),
+                                                                dev(I)), exact=exact)
+        res[exact] = host(A.data)
+    assert bits_equal(res[True], ref)
+    hot = counts[1:] > 512
+    assert bits_equal(res[False][~hot], ref[~hot])
+    # Tolerance for the reassociated hot-column sums: 1e-6 relative to the magnitude of
+    # the computation's inputs, |w| + eta * sum_k |delta_k| (the summation error bound
+    # scale; the serial fp32 sum itself is only that accurate).
+    absacc = np.zeros((ncols, dim), np.float64)
+    np.add.at(absacc, I.ravel() - 1, np.repeat(np.abs(delta).astype(np.float64), P, axis=0))
+    scale = np.abs(base.astype(np.float64)) + 0.1 * absacc
+    diff = np.abs(res[False].astype(np.float64) - ref)
+    assert np.all(diff <= 1e-6 * scale)
+    # deterministic: the chunked result repeats exactly
+    A = et.SimpleEmbedding(dev(base), et.Static(dim))
+    et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), dev(I)))
+    assert bits_equal(host(A.data), res[False])
+
+
+def test_update_partitions_exact(oracle):
+    """test/update.jl:90-120: 4 IndexerView splits give exactly the unsplit update."""
+    rng = np.random.default_rng(11)
+    base = rng.standard_normal((100, 16)).astype(np.float32)
+    delta = rng.standard_normal((512, 16)).astype(np.float32)
+    I = rng.integers(1, 101, 512)
+    for ixcls in (et.SparseIndexer, et.DenseIndexer):
+        A = et.SimpleEmbedding(dev(base), et.Static(16))
+        g = et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), dev(I))
+        ix = et.index_(ixcls(), g.indices, 100)
+        et.update_(A, g, ix, 1.0)
+        Bt = et.SimpleEmbedding(dev(base), et.Static(16))
+        for s in range(1, 5):
+            et.update_(Bt, g, et.IndexerView(ix, 4, s), 1.0)
+        assert bits_equal(host(A.data), host(Bt.data))
+        ref = base.copy()
+        oracle.sgd(ref, delta, I, 1.0, fused=True)
+        assert bits_equal(host(A.data), ref)
+
+
+@pytest.mark.parametrize("fused_dims", [(128, 128, 64), (16, 256, 80)])
+def test_multi_table_update_vs_oracle(oracle, fused_dims):
+    """Multi-table update! (src/sparseupdate.jl:199-238) through Preallocation grads
+    (strided deltas, ld = k + sum D), Static and Dynamic tables mixed."""
+    rng = np.random.default_rng(sum(fused_dims))
+    k, B, P = 8, 256, 20
+    rows = [300, 1000, 50]
+    hs = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, fused_dims)]
+    statics = [True, True, False]
+    tabs = [et.SimpleEmbedding(dev(h), et.Static(h.shape[1]) if s else et.Dynamic)
+            for h, s in zip(hs, statics)]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    y, back = et.rrule(et.maplookup, et.PreallocationStrategy(k), tabs, [dev(i) for i in hidx])
+    delta = rng.standard_normal(tuple(y.shape)).astype(np.float32)
+    grads = back(dev(delta))[2]
+    et.update_(et.Descent(0.1), tabs, grads, [et.Indexer() for _ in tabs])
+    from embtab.tables import fused_update_path
+
+    refs = [h.copy() for h in hs]
+    offs = np.cumsum([k] + list(fused_dims[:-1]))
+    oracle.sgd_multi(refs, delta, hidx, 0.1, [fused_update_path(t) for t in tabs], num_splits=4,
+                     nthreads=4, delta_offsets=offs)
+    for t in range(3):
+        assert bits_equal(host(tabs[t].data), refs[t]), f"table {t}"
+
+
+def test_map_gradients_structure():
+    """test/map.jl:530-589: grads through maplookup and PreallocationStrategy (with and
+    without prepended rows) carry the forward indices and equal deltas."""
+    rng = np.random.default_rng(0)
+    dims = [(5, 5), (5, 10), (5, 15)]
+    tabs = [et.SimpleEmbedding(dev(rng.random((c, d), dtype=np.float32))) for d, c in dims]
+    I = [dev(rng.integers(1, c + 1, 5)) for _, c in dims]
+    y, back = et.rrule(et.maplookup, et.DefaultStrategy(), tabs, I)
+    deltas = [torch.randn_like(o) for o in y]
+    g1 = back(deltas)[2]
+    for k in (0, 20):
+        yp, backp = et.rrule(et.maplookup, et.PreallocationStrategy(k), tabs, I)
+        big = torch.zeros_like(yp)
+        big[:, k:] = torch.cat(deltas, 1)
+        g2 = backp(big)[2]
+        for a, b, i in zip(g1, g2, I):
+            assert isinstance(b, et.SparseEmbeddingUpdate)
+            assert b.indices is i and a.indices is i
+            assert torch.equal(a.delta, b.delta)
+
+
+def test_update_oob_skipped():
+    et.check_errors()
+    A = et.SimpleEmbedding(torch.zeros((10, 16), dtype=torch.float32, device=DEV), et.Static(16))
+    I = torch.tensor([1, 11, 2], dtype=torch.int64, device=DEV)
+    d = torch.ones((3, 16), dtype=torch.float32, device=DEV)
+    et.update_(et.Descent(1.0), A, et.SparseEmbeddingUpdate(A.lookup_type, d, I))
+    assert et.check_errors() == 1
+    out = host(A.data)
+    assert (out[0] == -1).all() and (out[1] == -1).all() and not out[2:].any()

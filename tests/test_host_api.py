@@ -1,0 +1,68 @@
+"""Host-side mirror of the reference API that runs without a GPU: constructors
+(test/constructors.jl), dispatch rules, index containers, IndexerView ranges, and
+that the product path refuses to compute on the CPU (no silent fallback)."""
+import pytest
+import torch
+
+import embtab as et
+
+
+def test_constructors():
+    """test/constructors.jl:1-25."""
+    even = torch.rand(10, 64)  # Julia 64 x 10
+    odd = torch.rand(10, 65)
+    x = et.SimpleEmbedding(even, et.Static(64))
+    assert x.size() == (64, 10)
+    with pytest.raises(et.ArgumentError):
+        et.SimpleEmbedding(even, et.Static(32))
+    with pytest.raises(et.ArgumentError):
+        et.Static(64.0)
+    x = et.SimpleEmbedding(odd)
+    assert x.size() == (65, 10) and x.lookup_type is et.Dynamic
+    x = et.SimpleEmbedding(odd, et.Static(65))
+    assert x.lookup_type == et.Static(65)
+
+
+def test_columnpointer_and_example():
+    data = torch.rand(10, 16)
+    A = et.SimpleEmbedding(data, et.Static(16))
+    assert A.columnpointer(1) == data.data_ptr()
+    assert A.columnpointer(3) == data.data_ptr() + 2 * 16 * 4
+    assert et.example(A) is data and et.featuresize(A) == 16
+    assert et.example([A]) is data
+    assert A[2, 3] == pytest.approx(float(data[2, 1]))
+    A[2, 3] = 5.0
+    assert float(data[2, 1]) == 5.0
+
+
+def test_fused_path_dispatch_rule():
+    """src/sparseupdate.jl:131-154: specialized iff Static and N*sizeof(T) <= 512."""
+    from embtab.tables import fused_update_path
+
+    assert fused_update_path(et.SimpleEmbedding(torch.rand(3, 128), et.Static(128)))
+    assert not fused_update_path(et.SimpleEmbedding(torch.rand(3, 256), et.Static(256)))
+    assert not fused_update_path(et.SimpleEmbedding(torch.rand(3, 128)))
+
+
+def test_colwrap():
+    I = torch.arange(2 * 5 * 3).reshape(3, 5, 2)  # Julia 2 x 5 x 3
+    parts = et.colwrap(I)
+    assert len(parts) == 3 and parts[1].shape == (5, 2)
+    assert et.colwrap([I[0], I[1]])[1] is I[1] or torch.equal(et.colwrap([I[0], I[1]])[1], I[1])
+
+
+def test_indexer_view_ranges():
+    """src/utils.jl:325-333 on an Indexer with U = 6 distinct columns (7 cumulative)."""
+    ix = et.Indexer()
+    ix.cumulative = torch.zeros((7, 2), dtype=torch.int64)
+    ranges = [et.IndexerView(ix, 4, s).entries() for s in range(1, 5)]
+    assert ranges == [(0, 2), (2, 4), (4, 6), (6, 6)]
+    covered = [e for b, f in ranges for e in range(b, f)]
+    assert covered == list(range(6))
+
+
+def test_no_cpu_fallback():
+    """The product path computes on the GPU only: CPU tensors are refused loudly."""
+    A = et.SimpleEmbedding(torch.rand(10, 16), et.Static(16))
+    with pytest.raises(et.ArgumentError):
+        et.lookup(A, torch.tensor([1, 2, 3]))
