@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""Benchmark of the embedding-table hot path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the metric's config): 26 fp32 tables of dim
+128 with Criteo-Kaggle cardinalities (public DLRM statistics, NOT from the
+reference — labelled as such), matrix-index pooled sum with pool 20, batch 65536,
+PreallocationStrategy(0).  A step is one fused maplookup of the whole batch over
+all 26 tables (one kernel launch at N = 1), inputs resident in HBM.
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): the tables are split
+table-wise over the ranks (4,4,3,3,3,3,3,3 at N = 8); a step is each rank's fused
+lookup of its tables + the RCCL all-gather of the slabs + the concat assembly, so
+the whole-job throughput is B*T*P lookups per step time ("scaling": "strong").
+
+Prints ONE JSON line on rank 0 with the roofline of the dominant kernel
+(k_pooled_vec, HIP events on the launch stream) and the CPU baseline (the oracle's
+multithreaded restatement of the reference CPU path, timed on this host's cores on
+the same tables and indices, with its output compared bit-for-bit to the GPU's).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "embeddingtables.jl_amd"))
+
+# Criteo-Kaggle (DLRM) cardinalities — public statistics, not from the reference.
+CRITEO_KAGGLE_ROWS = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683,
+                      8351593, 3194, 27, 14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15,
+                      286181, 105, 142572]
+DIM, POOL, BATCH = 128, 20, 65536
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+TABLE_SEED, INDEX_SEED = 1000, 2000
+
+
+def algorithmic_bytes(batch, ntables, pool, dims, es=4):
+    """Per launch: every gathered row + every index + every output element
+    (SURVEY.md §8d)."""
+    return batch * ntables * pool * DIM * es + batch * ntables * pool * 8 + batch * sum(dims) * es
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=BATCH)
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="target CPU-baseline sample duration (0 disables)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or 16")
+    p.add_argument("--no-check", action="store_true", help="skip the CPU/GPU bit comparison")
+    return p.parse_args()
+
+
+def make_tables(et, L, tids, device):
+    import torch
+    from embtab import _lib
+
+    tables, idx = [], []
+    stream = _lib.stream_handle(device)
+    for t in tids:
+        R = CRITEO_KAGGLE_ROWS[t]
+        data = torch.empty((R, DIM), dtype=torch.float32, device=device)
+        _lib.check(L.et_fill_uniform(_lib.ET_F32, data.data_ptr(), data.numel(), TABLE_SEED + t, 0,
+                                     0.0, 1.0, stream))
+        tables.append(et.SimpleEmbedding(data, et.Static(DIM)))
+    return tables
+
+
+def make_indices(L, tids, batch, device):
+    import torch
+    from embtab import _lib
+
+    stream = _lib.stream_handle(device)
+    idx = []
+    for t in tids:
+        I = torch.empty((batch, POOL), dtype=torch.int64, device=device)
+        _lib.check(L.et_fill_index_uniform(I.data_ptr(), I.numel(), CRITEO_KAGGLE_ROWS[t],
+                                           INDEX_SEED + t, 0, stream))
+        idx.append(I)
+    return idx
+
+
+def cpu_baseline(gpu_out, idx, batch, seconds, threads, check):
+    """Time the oracle's Preallocation maplookup (reference CPU algorithm, C + pthreads,
+    atomic work queue with worksize_div = 8) on host copies of the same inputs."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as orc
+
+    t0 = time.time()
+    tabs = [orc.fill_uniform((R, DIM), np.float32, TABLE_SEED + t, 0, 0.0, 1.0, nthreads=threads)
+            for t, R in enumerate(CRITEO_KAGGLE_ROWS)]
+    hidx = [i.cpu().numpy() for i in idx]
+    setup = time.time() - t0
+    out = np.empty((batch, len(tabs) * DIM), np.float32)
+    # one untimed pass (page-in), then whole steps until the time budget is spent
+    orc.maplookup_prealloc(tabs, hidx, nthreads=threads, out=out)
+    same = None
+    if check:
+        same = bool(np.array_equal(out, gpu_out))
+    steps, t0 = 0, orc.now()
+    while True:
+        orc.maplookup_prealloc(tabs, hidx, nthreads=threads, out=out)
+        steps += 1
+        el = orc.now() - t0
+        if el >= seconds or steps >= 50:
+            break
+    lookups = steps * batch * len(tabs) * POOL
+    return {
+        "value": lookups / el,
+        "unit": "lookups/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{steps} full step(s) of the same workload ({batch} bags x {len(tabs)} tables "
+                  f"x pool {POOL}, same tables and indices) in {el:.2f} s; C restatement of "
+                  "src/lookup.jl:316-371 + :134-165 (oracle/embtab_oracle.c), pthreads atomic "
+                  "work queue, worksize_div 8",
+        "ms_per_step": 1e3 * el / steps,
+        "gpu_output_bit_identical": same,
+        "setup_s": round(setup, 2),
+    }
+
+
+def load_traffic():
+    path = os.path.join(REPO, "profiles", "traffic_r01.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import embtab as et
+    from embtab import _lib
+    from embtab.sharding import ShardLayout, ShardedPreallocation, plan_tables
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("run N>1 under torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    L = _lib.load()
+    B = args.batch
+    T = len(CRITEO_KAGGLE_ROWS)
+    dims = [DIM] * T
+    assignment = plan_tables(T, world)
+    mine = assignment[rank]
+    tables = make_tables(et, L, mine, device)
+    idx = make_indices(L, mine, B, device)
+    layout = ShardLayout(dims, 0, assignment)
+    dst = torch.empty((B, layout.ld), dtype=torch.float32, device=device)
+    strat = et.PreallocationStrategy(0)
+    sharded = ShardedPreallocation(layout, rank, world, B, torch.float32, device) \
+        if world > 1 else None
+
+    def step():
+        if sharded is None:
+            et.maplookup_(strat, dst, tables, idx)
+        else:
+            sharded(tables, idx, dst)
+
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # kernel-level timing of the dominant launch on the stream it runs on
+    stream = torch.cuda.current_stream(device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        if sharded is None:
+            ev[k][0].record(stream)
+            et.maplookup_(strat, dst, tables, idx)
+            ev[k][1].record(stream)
+        else:
+            ev[k][0].record(stream)
+            sharded.local_lookup(tables, idx)
+            ev[k][1].record(stream)
+            sharded.exchange()
+            sharded.assemble(dst)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    lookups_per_step = B * T * POOL
+    value = lookups_per_step * args.steps / elapsed
+    local_bytes = algorithmic_bytes(B, len(mine), POOL, [DIM] * len(mine))
+    achieved = local_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic()
+    traffic_bytes = None
+    if traffic and traffic.get("workload") == f"criteo26_b{B}" and world == 1:
+        traffic_bytes = traffic.get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": "embedding lookups/sec + achieved HBM GB/s (% of roofline), 26 tables x dim128 "
+                  "at B=65536",
+        "value": value,
+        "unit": "lookups/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: counter-hash uniform[0,1) fp32 tables, uniform 1-based Int64 indices "
+                "(seeded, identical on CPU and GPU)",
+        "config": {
+            "workload": "criteo-kaggle 26 tables x dim 128 fp32, pooled sum pool 20, "
+                        "PreallocationStrategy(0)",
+            "global_batch": B,
+            "tables": T,
+            "pool": POOL,
+            "dim": DIM,
+            "table_rows": CRITEO_KAGGLE_ROWS,
+            "parallelism": "single GPU" if world == 1 else f"table-wise x{world} + RCCL all-gather",
+        },
+        "bags_per_s": B * T * args.steps / elapsed,
+        "samples_per_s": B * args.steps / elapsed,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_pooled_vec<float,float,128,8,NT>",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic_bytes,
+            "algorithmic_bytes_per_launch": local_bytes,
+            "kernel_ms": kernel_ms,
+        },
+    }
+    if world > 1:
+        result["lookup_only_ms"] = kernel_ms
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 16)
+        threads = max(1, min(threads, os.cpu_count() or 1))
+        gpu_out = None if args.no_check else dst.cpu().numpy()
+        result["cpu_baseline"] = cpu_baseline(gpu_out, idx, B, args.cpu_seconds, threads,
+                                              not args.no_check)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

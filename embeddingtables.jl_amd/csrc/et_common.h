@@ -67,7 +67,7 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // Out-of-range index counter (read + cleared by et_check_errors).
 __device__ unsigned long long g_oob_count;
 
-__device__ __forceinline__ void note_oob() { atomicAdd(&g_oob_count, 1ull); }
+__device__ __forceinline__ void note_oob(int n = 1) { atomicAdd(&g_oob_count, (unsigned long long)n); }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 

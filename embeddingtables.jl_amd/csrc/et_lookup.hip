@@ -62,7 +62,7 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint64_t l
                                          uint64_t nrows, long long my, int gbase, int sub,
                                          int i0, bool first_batch,
                                          A (&acc)[VecGeom<T, D>::NV][VecGeom<T, D>::N],
-                                         bool& bad) {
+                                         int& bad) {
     using G = VecGeom<T, D>;
     constexpr int N = G::N, LPR = G::LPR, NV = G::NV;
     uint64_t off[UU];
@@ -83,7 +83,7 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint64_t l
     }
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        bad |= !ok[u];
+        bad += ok[u] ? 0 : 1;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             T x[N];
@@ -117,7 +117,7 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, int64_t
     for (int v = 0; v < NV; ++v)
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[v][k] = A(0);
-    bool bad = false;
+    int bad = 0;  // out-of-range indices of this bag (same in every lane of the group)
     const uint64_t ldt = (uint64_t)ld_table, nr = (uint64_t)nrows;
 
     for (int c0 = 0; c0 < pool; c0 += LPR) {
@@ -143,7 +143,7 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, int64_t
         if (cnt - i0 >= 1)
             load_add<T, A, D, 1>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
     }
-    if (bad) note_oob();
+    if (bad && sub == 0) note_oob(bad);
     u32x4* o = reinterpret_cast<u32x4*>(out) + sub;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -218,12 +218,12 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
 #pragma unroll
             for (int v = 0; v < NV; ++v) buf[u][v] = src[v * LPR];
         }
-        bool bad = false;
+        int bad = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t bag = bag0 + u * per_round;
             if (bag < batch) {
-                bad |= !okv[u];
+                bad += okv[u] ? 0 : 1;
                 u32x4* o =
                     reinterpret_cast<u32x4*>(dst + bag * ld_dst_b + d.dst_row_off * es) + sub;
 #pragma unroll
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
                     store16<NT>(o + v * LPR, okv[u] ? buf[u][v] : u32x4{0u, 0u, 0u, 0u});
             }
         }
-        if (bad) note_oob();
+        if (bad && sub == 0) note_oob(bad);
     }
 }
 
