@@ -109,7 +109,7 @@ def cpu_baseline(gpu_out, idx, batch, seconds, threads, check):
         orc.maplookup_prealloc(tabs, hidx, nthreads=threads, out=out)
         steps += 1
         el = orc.now() - t0
-        if el >= seconds or steps >= 50:
+        if el >= seconds or steps >= 1000:
             break
     lookups = steps * batch * len(tabs) * POOL
     return {

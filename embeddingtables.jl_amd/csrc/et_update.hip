@@ -88,7 +88,8 @@ __global__ __launch_bounds__(256) void k_seg_start(const uint32_t* __restrict__ 
     const bool head = (i == 0 || keys[i] != keys[i - 1]);
     if (head) seg_start[segid[i]] = (uint32_t)i;
     if (i == n - 1) {
-        const uint32_t U = segid[i] + 1u;
+        // segid is the EXCLUSIVE scan of the head flags: U = heads before + this head
+        const uint32_t U = segid[i] + (head ? 1u : 0u);
         seg_start[U] = (uint32_t)n;
         counters[kCntU] = U;
     }

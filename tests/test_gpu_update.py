@@ -113,14 +113,22 @@ def test_update_hot_rows_chunked_vs_exact(oracle):
     assert bits_equal(res[True], ref)
     hot = counts[1:] > 512
     assert bits_equal(res[False][~hot], ref[~hot])
-    # Tolerance for the reassociated hot-column sums: 1e-6 relative to the magnitude of
-    # the computation's inputs, |w| + eta * sum_k |delta_k| (the summation error bound
-    # scale; the serial fp32 sum itself is only that accurate).
+    # Tolerance for the reassociated hot-column sums, measured against the EXACT (fp64)
+    # update: 1e-6 relative to the magnitude of the computation's inputs,
+    # |w| + eta * sum_k |delta_k| (the summation error-bound scale).  The reference's own
+    # serial fp32 sum is only about that accurate on a 50k-occurrence column; the chunked
+    # sum is measured at ~10x closer to exact there (scratch diagnostics).
+    acc = np.zeros((ncols, dim), np.float64)
+    np.add.at(acc, I.ravel() - 1, np.repeat(delta.astype(np.float64), P, axis=0))
     absacc = np.zeros((ncols, dim), np.float64)
     np.add.at(absacc, I.ravel() - 1, np.repeat(np.abs(delta).astype(np.float64), P, axis=0))
-    scale = np.abs(base.astype(np.float64)) + 0.1 * absacc
-    diff = np.abs(res[False].astype(np.float64) - ref)
-    assert np.all(diff <= 1e-6 * scale)
+    eta = np.float64(np.float32(0.1))
+    exact_upd = base.astype(np.float64) - eta * acc
+    scale = np.abs(base.astype(np.float64)) + eta * absacc
+    err_chunked = np.abs(res[False].astype(np.float64) - exact_upd)
+    err_serial = np.abs(ref.astype(np.float64) - exact_upd)
+    assert np.all(err_chunked <= 1e-6 * scale)
+    assert err_chunked[hot].max() <= err_serial[hot].max()
     # deterministic: the chunked result repeats exactly
     A = et.SimpleEmbedding(dev(base), et.Static(dim))
     et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), dev(I)))
