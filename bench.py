@@ -53,6 +53,8 @@ def parse():
                    help="target CPU-baseline sample duration (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or 16")
     p.add_argument("--no-check", action="store_true", help="skip the CPU/GPU bit comparison")
+    p.add_argument("--rows", type=int, default=0,
+                   help="calibration only: give every table this many rows (0 = Criteo)")
     return p.parse_args()
 
 
@@ -145,6 +147,8 @@ def main():
     from embtab import _lib
     from embtab.sharding import ShardLayout, ShardedPreallocation, plan_tables
 
+    if args.rows:
+        CRITEO_KAGGLE_ROWS[:] = [args.rows] * len(CRITEO_KAGGLE_ROWS)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

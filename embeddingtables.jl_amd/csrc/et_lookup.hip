@@ -21,6 +21,9 @@
 //     allocation, hipGraph-capturable).
 #include "et_common.h"
 
+#include <stdlib.h>
+#include <string.h>
+
 namespace et {
 
 struct LookupPack {
@@ -53,14 +56,45 @@ __device__ __forceinline__ u32x4 pack16(const T (&x)[N]) {
     return v;
 }
 
-// Issue UU row loads of one bag (slots i0 .. i0+UU-1 of the current index chunk,
-// all valid), then add them to the accumulator in slot order.  Straight-line code:
-// every load is issued before the first add waits, so UU rows per group are in
-// flight (the waitcnt pass counts vmcnt down through the adds).
-template <typename T, typename A, int D, int UU>
-__device__ __forceinline__ void load_add(const T* __restrict__ table, uint64_t ld_table,
-                                         uint64_t nrows, long long my, int gbase, int sub,
-                                         int i0, bool first_batch,
+// Broadcast the 64-bit value held by lane (g*LPR + i) to every lane of group g; i is
+// wave-uniform.  With <= 4 groups per wave this is 2*GPW v_readlane + selects (no LDS
+// round trip, nothing for the waitcnt pass to serialise); wider waves use ds_bpermute.
+template <int LPR>
+__device__ __forceinline__ long long group_bcast(long long v, int i, int g) {
+    constexpr int GPW = 64 / LPR;
+    if constexpr (GPW <= 4) {
+        const int lo = (int)v, hi = (int)(v >> 32);
+        int rlo = __builtin_amdgcn_readlane(lo, i), rhi = __builtin_amdgcn_readlane(hi, i);
+#pragma unroll
+        for (int gg = 1; gg < GPW; ++gg) {
+            const int tlo = __builtin_amdgcn_readlane(lo, gg * LPR + i);
+            const int thi = __builtin_amdgcn_readlane(hi, gg * LPR + i);
+            rlo = g == gg ? tlo : rlo;
+            rhi = g == gg ? thi : rhi;
+        }
+        return (long long)(((unsigned long long)(unsigned)rhi << 32) | (unsigned)rlo);
+    } else {
+        return __shfl(v, g * LPR + i, 64);
+    }
+}
+
+// The first (up to) LPR indices of a bag, one per lane of the group; lanes past the
+// end re-read the last one so that no lane is masked off.
+template <int LPR>
+__device__ __forceinline__ long long load_idx_chunk(const int64_t* __restrict__ ip, int cnt,
+                                                    int sub) {
+    return (long long)ip[sub < cnt ? sub : cnt - 1];
+}
+
+// Issue UU row loads of one bag (slots i0 .. i0+UU-1 of the current index chunk, all
+// valid), then add them to the accumulator in slot order.  Straight-line code: every
+// load is issued before the first add waits, so UU rows per group are in flight (the
+// waitcnt pass counts vmcnt down through the adds).  Row offsets use one 32x32->64
+// multiply (the host guarantees nrows and ld_table below 2^32).
+template <typename T, typename A, int D, int UU, bool NTL>
+__device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t ld_table,
+                                         uint32_t nrows, long long my, int g, int sub, int i0,
+                                         bool first_batch,
                                          A (&acc)[VecGeom<T, D>::NV][VecGeom<T, D>::N],
                                          int& bad) {
     using G = VecGeom<T, D>;
@@ -69,17 +103,22 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint64_t l
     bool ok[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const long long r = __shfl(my, gbase + i0 + u, 64);
+        const long long r = group_bcast<LPR>(my, i0 + u, g);
         const uint64_t row = (uint64_t)(r - 1);
-        ok[u] = row < nrows;
-        off[u] = ok[u] ? row * ld_table : 0;
+        ok[u] = row < (uint64_t)nrows;
+        off[u] = ok[u] ? (uint64_t)(uint32_t)row * ld_table : 0;
     }
     u32x4 buf[UU][NV];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         const u32x4* src = reinterpret_cast<const u32x4*>(table + off[u]) + sub;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) buf[u][v] = src[v * LPR];
+        for (int v = 0; v < NV; ++v) {
+            if constexpr (NTL)
+                buf[u][v] = __builtin_nontemporal_load(src + v * LPR);
+            else
+                buf[u][v] = src[v * LPR];
+        }
     }
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
@@ -100,16 +139,17 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint64_t l
 }
 
 // Pooled sum of one bag by one lane group (vector path).
-//   ip  : the bag's index list (1-based), `pool` entries
+//   ip  : the bag's index list (1-based), `pool` >= 1 entries
+//   my0 : its first index chunk, already loaded (load_idx_chunk)
 //   out : the bag's output column
-//   sub : lane within the group, gbase : first lane of the group in the wave
 // Accumulation is acc = row(I[1]); acc += row(I[i]) for i = 2..P, element-wise and in
 // order (src/lookup.jl:139-146), so fp32/fp64/int results equal the reference bit
 // for bit; F16 rounds after every add (Julia Float16 `+`) unless A = float.
-template <typename T, typename A, int D, int U, bool NT>
-__device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, int64_t ld_table,
-                                            int64_t nrows, const int64_t* __restrict__ ip,
-                                            int pool, T* __restrict__ out, int sub, int gbase) {
+template <typename T, typename A, int D, int U, bool NT, bool NTL>
+__device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_t ld_table,
+                                            uint32_t nrows, const int64_t* __restrict__ ip,
+                                            int pool, long long my0, T* __restrict__ out, int g,
+                                            int sub) {
     using G = VecGeom<T, D>;
     constexpr int N = G::N, LPR = G::LPR, NV = G::NV;
     A acc[NV][N];
@@ -118,30 +158,38 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, int64_t
 #pragma unroll
         for (int k = 0; k < N; ++k) acc[v][k] = A(0);
     int bad = 0;  // out-of-range indices of this bag (same in every lane of the group)
-    const uint64_t ldt = (uint64_t)ld_table, nr = (uint64_t)nrows;
 
     for (int c0 = 0; c0 < pool; c0 += LPR) {
         const int cnt = pool - c0 < LPR ? pool - c0 : LPR;
-        // One coalesced read of (up to) LPR indices of this bag; lanes past the end
-        // re-read the last one so that no lane is masked off.
-        const long long my = (long long)ip[c0 + (sub < cnt ? sub : cnt - 1)];
+        const long long my = c0 == 0 ? my0 : load_idx_chunk<LPR>(ip + c0, cnt, sub);
         int i0 = 0;
         for (; i0 + U <= cnt; i0 += U)
-            load_add<T, A, D, U>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+            load_add<T, A, D, U, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0, acc,
+                                      bad);
+        if constexpr (U > 8) {
+            if (cnt - i0 >= 8) {
+                load_add<T, A, D, 8, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0,
+                                          acc, bad);
+                i0 += 8;
+            }
+        }
         if constexpr (U > 4) {
             if (cnt - i0 >= 4) {
-                load_add<T, A, D, 4>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+                load_add<T, A, D, 4, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0,
+                                          acc, bad);
                 i0 += 4;
             }
         }
         if constexpr (U > 2) {
             if (cnt - i0 >= 2) {
-                load_add<T, A, D, 2>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+                load_add<T, A, D, 2, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0,
+                                          acc, bad);
                 i0 += 2;
             }
         }
         if (cnt - i0 >= 1)
-            load_add<T, A, D, 1>(table, ldt, nr, my, gbase, sub, i0, c0 + i0 == 0, acc, bad);
+            load_add<T, A, D, 1, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0, acc,
+                                      bad);
     }
     if (bad && sub == 0) note_oob(bad);
     u32x4* o = reinterpret_cast<u32x4*>(out) + sub;
@@ -154,26 +202,82 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, int64_t
     }
 }
 
+// `rounds` bags of one table per lane group, the next bag's first index chunk loaded
+// while the current bag's rows are in flight.
+template <typename T, typename A, int D, int U, bool NT, bool NTL>
+__device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
+                                         T* __restrict__ dst, int64_t ld_dst, int64_t chunk,
+                                         int rounds) {
+    using G = VecGeom<T, D>;
+    const T* table = reinterpret_cast<const T*>(d.table);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / G::LPR, sub = lane % G::LPR;
+    const int64_t per_round = 4 * G::GPW;
+    const int pool = d.pool;
+    const int cnt0 = pool < G::LPR ? pool : G::LPR;
+    const uint32_t ldt = (uint32_t)d.ld_table, nr = (uint32_t)d.nrows;
+    int64_t bag = chunk * per_round * rounds + wave * G::GPW + g;
+    long long my_next = load_idx_chunk<G::LPR>(
+        d.idx + (bag < batch ? bag : batch - 1) * d.ld_idx, cnt0, sub);
+    for (int r = 0; r < rounds; ++r) {
+        if (bag >= batch) break;
+        const long long my = my_next;
+        const int64_t nbag = bag + per_round;
+        if (r + 1 < rounds)
+            my_next = load_idx_chunk<G::LPR>(d.idx + (nbag < batch ? nbag : batch - 1) * d.ld_idx,
+                                             cnt0, sub);
+        bag_sum_vec<T, A, D, U, NT, NTL>(table, ldt, nr, d.idx + bag * d.ld_idx, pool, my,
+                                         dst + bag * ld_dst + d.dst_row_off, g, sub);
+        bag = nbag;
+    }
+}
+
 // Pooled-sum kernel, vector path: grid = ntables * nchunks workgroups of 256.
 template <typename T, typename A, int D, int U, bool NT>
 __global__ __launch_bounds__(256) void k_pooled_vec(LookupPack pack, int ntables, int64_t batch,
                                                     T* __restrict__ dst, int64_t ld_dst,
                                                     int rounds) {
-    using G = VecGeom<T, D>;
     const int64_t item = blockIdx.x;
     const int t = (int)(item % ntables);
     const int64_t chunk = item / ntables;
-    const et_lookup_desc& d = pack.d[t];
-    const T* table = reinterpret_cast<const T*>(d.table);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int g = lane / G::LPR, sub = lane % G::LPR;
-    const int64_t per_round = 4 * G::GPW;
-    int64_t bag = chunk * per_round * rounds + wave * G::GPW + g;
-    for (int r = 0; r < rounds; ++r, bag += per_round) {
-        if (bag >= batch) break;
-        bag_sum_vec<T, A, D, U, NT>(table, d.ld_table, d.nrows, d.idx + bag * d.ld_idx, d.pool,
-                                 dst + bag * ld_dst + d.dst_row_off, sub, g * G::LPR);
-    }
+    run_bags<T, A, D, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+}
+
+// XCD-aware stripe schedule for multi-table launches.  Every table's chunks are cut
+// into kXcds stripes; XCD x owns `ntables` stripes: one stripe of every HEAVY table
+// (too big for an L2, so its rows come from HBM / the Infinity Cache whoever reads
+// them) and whole runs of the LIGHT tables' stripes, so each XCD's 4 MiB L2 only
+// ever holds a couple of light tables.  Workgroup b runs on XCD b % 8 (the observed
+// round-robin dispatch; a different placement changes speed only, never results),
+// and consecutive workgroups of one XCD cycle through its stripes, mixing HBM-bound
+// and L2-bound work in time.
+constexpr int kXcds = 8;
+
+// 32-bit entries (table | stripe << 8) so the map is read with scalar loads (gfx950
+// has no scalar byte loads).
+struct StripeMap {
+    uint32_t entry[kXcds][ET_MAX_TABLES_PER_LAUNCH];
+    uint32_t ntload_mask;  // bit t: non-temporal row loads for table t
+};
+
+template <typename T, typename A, int D, int U, bool NT>
+__global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, StripeMap sm,
+                                                            int ntables, int64_t batch,
+                                                            T* __restrict__ dst, int64_t ld_dst,
+                                                            int rounds, int64_t stripe_chunks,
+                                                            int64_t nchunks) {
+    const int x = blockIdx.x % kXcds;
+    const int64_t slot = blockIdx.x / kXcds;
+    const int k = (int)(slot % ntables);
+    const int64_t j = slot / ntables;
+    const uint32_t e = sm.entry[x][k];
+    const int t = (int)(e & 0xff);
+    const int64_t chunk = (int64_t)(e >> 8) * stripe_chunks + j;
+    if (j >= stripe_chunks || chunk >= nchunks) return;
+    if ((sm.ntload_mask >> t) & 1u)
+        run_bags<T, A, D, U, NT, true>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    else
+        run_bags<T, A, D, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
 }
 
 // Non-reducing gather (bit copy) of RB-byte rows: each group moves U rows at once.
@@ -306,17 +410,104 @@ inline int rounds_for(int64_t batch, int64_t bags_per_round, int ntables) {
     return rounds;
 }
 
+// Scheduling knobs (read once; for experiments — the defaults are the tuned choice).
+struct LookupTuning {
+    int striped = 1;               // ET_SCHED=linear disables the XCD stripe schedule
+    int ntload = 0;                // ET_NTLOAD=1: non-temporal row loads of heavy tables
+    int64_t light_bytes = 4 << 20; // tables up to one XCD L2 (4 MiB) are "light"
+    int rows_in_flight = 0;        // ET_U=4|8|16: rows per group in flight (fp32 D=128)
+};
+
+inline const LookupTuning& tuning() {
+    static LookupTuning t = [] {
+        LookupTuning v;
+        if (const char* e = getenv("ET_SCHED")) v.striped = strcmp(e, "linear") != 0;
+        if (const char* e = getenv("ET_NTLOAD")) v.ntload = atoi(e);
+        if (const char* e = getenv("ET_LIGHT_BYTES")) v.light_bytes = atoll(e);
+        if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
+        return v;
+    }();
+    return t;
+}
+
+// Stripe assignment: heavy tables -> stripe x on XCD x; light tables' stripes laid out
+// table after table (alternating large and small tables) and cut into kXcds equal runs.
+inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& sm) {
+    const LookupTuning& tu = tuning();
+    int heavy[ET_MAX_TABLES_PER_LAUNCH], light[ET_MAX_TABLES_PER_LAUNCH];
+    int nh = 0, nl = 0;
+    int64_t bytes[ET_MAX_TABLES_PER_LAUNCH];
+    sm.ntload_mask = 0;
+    for (int t = 0; t < n; ++t) {
+        bytes[t] = pack.d[t].nrows * pack.d[t].ld_table * es;
+        if (bytes[t] > tu.light_bytes) {
+            heavy[nh++] = t;
+            if (tu.ntload) sm.ntload_mask |= 1u << t;
+        } else {
+            light[nl++] = t;
+        }
+    }
+    // light tables by size, then interleave large / small
+    for (int a = 0; a < nl; ++a)
+        for (int b = a + 1; b < nl; ++b)
+            if (bytes[light[b]] > bytes[light[a]]) {
+                int tmp = light[a];
+                light[a] = light[b];
+                light[b] = tmp;
+            }
+    int order[ET_MAX_TABLES_PER_LAUNCH];
+    for (int i = 0, lo = 0, hi = nl - 1; i < nl; ++i) order[i] = (i & 1) ? light[hi--] : light[lo++];
+    int cnt[kXcds] = {0};
+    for (int x = 0; x < kXcds; ++x)
+        for (int h = 0; h < nh; ++h) sm.entry[x][cnt[x]++] = (uint32_t)heavy[h] | ((uint32_t)x << 8);
+    // linear list of light stripes (order[i], st), st < kXcds; XCD x takes [x*nl, (x+1)*nl)
+    for (int q = 0; q < nl * kXcds; ++q) {
+        const int x = q / (nl > 0 ? nl : 1);
+        sm.entry[x][cnt[x]++] = (uint32_t)order[q / kXcds] | ((uint32_t)(q % kXcds) << 8);
+    }
+}
+
+template <typename T, typename A, int D, int U, bool NT>
+int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
+                        hipStream_t s);
+
 template <typename T, typename A, int D, bool NT>
 int launch_pooled_vec(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                       hipStream_t s) {
+    if constexpr (D == 128 && __is_same(T, float)) {
+        switch (tuning().rows_in_flight) {
+            case 4: return launch_pooled_vec_u<T, A, D, 4, NT>(pack, n, batch, dst, ld_dst, s);
+            case 16: return launch_pooled_vec_u<T, A, D, 16, NT>(pack, n, batch, dst, ld_dst, s);
+            default: break;
+        }
+    }
+    return launch_pooled_vec_u<T, A, D, VecGeom<T, D>::U, NT>(pack, n, batch, dst, ld_dst, s);
+}
+
+template <typename T, typename A, int D, int U, bool NT>
+int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
+                        hipStream_t s) {
     using G = VecGeom<T, D>;
     const int64_t per_round = 4 * G::GPW;
     const int rounds = rounds_for(batch, per_round, n);
     const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
+    if (nchunks <= 0) return ET_OK;
+    if (n > 1 && tuning().striped) {
+        StripeMap sm;
+        build_stripe_map(pack, n, (int)sizeof(T), sm);
+        const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
+        const int64_t grid = (int64_t)kXcds * n * stripe_chunks;
+        if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+        hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT>), dim3((unsigned)grid),
+                           dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst), ld_dst,
+                           rounds, stripe_chunks, nchunks);
+        ET_LAUNCH_CHECK("k_pooled_vec_striped");
+        return ET_OK;
+    }
     const int64_t grid = nchunks * n;
     if (grid <= 0) return ET_OK;
     if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
-    hipLaunchKernelGGL((k_pooled_vec<T, A, D, G::U, NT>), dim3((unsigned)grid), dim3(256), 0, s, pack,
+    hipLaunchKernelGGL((k_pooled_vec<T, A, D, U, NT>), dim3((unsigned)grid), dim3(256), 0, s, pack,
                        n, batch, reinterpret_cast<T*>(dst), ld_dst, rounds);
     ET_LAUNCH_CHECK("k_pooled_vec");
     return ET_OK;
@@ -462,7 +653,8 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
             kind_of[t] = -1;
         } else if (d.pool == 1 && al && gather_rb_ok((int64_t)d.dim * es)) {
             kind_of[t] = kGather;
-        } else if (d.pool >= 1 && al && vec_dim_ok(d.dim)) {
+        } else if (d.pool >= 1 && al && vec_dim_ok(d.dim) && d.nrows < 0xffffffffll &&
+                   d.ld_table < 0xffffffffll) {
             kind_of[t] = kPooledVec;
         } else {
             kind_of[t] = kGeneric;
