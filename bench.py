@@ -53,6 +53,8 @@ def parse():
                    help="target CPU-baseline sample duration (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or 16")
     p.add_argument("--no-check", action="store_true", help="skip the CPU/GPU bit comparison")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the config-2 (gather) and config-4 (Zipf + SGD) measurements")
     p.add_argument("--rows", type=int, default=0,
                    help="calibration only: give every table this many rows (0 = Criteo)")
     return p.parse_args()
@@ -127,6 +129,109 @@ def cpu_baseline(gpu_out, idx, batch, seconds, threads, check):
         "gpu_output_bit_identical": same,
         "setup_s": round(setup, 2),
     }
+
+
+def _timed(fn, steps, warmup, stream):
+    """Average HIP-event time (ms) of fn() on `stream` over `steps` launches."""
+    import torch
+
+    for _ in range(warmup):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize()
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / steps
+
+
+def bench_config2(et, L, device, steps, warmup):
+    """BASELINE configs[1]: one 128 x 1e7 fp32 table, vector-index (non-reducing) gather,
+    B = 65536.  Bytes per lookup: 512 read + 512 written + 8 index."""
+    import torch
+    from embtab import _lib
+
+    R, B = 10_000_000, BATCH
+    stream = torch.cuda.current_stream(device)
+    data = torch.empty((R, DIM), dtype=torch.float32, device=device)
+    _lib.check(L.et_fill_uniform(_lib.ET_F32, data.data_ptr(), data.numel(), 3000, 0, 0.0, 1.0,
+                                 stream.cuda_stream))
+    I = torch.empty(B, dtype=torch.int64, device=device)
+    _lib.check(L.et_fill_index_uniform(I.data_ptr(), B, R, 3001, 0, stream.cuda_stream))
+    A = et.SimpleEmbedding(data, et.Static(DIM))
+    dst = torch.empty((B, DIM), dtype=torch.float32, device=device)
+    ms = _timed(lambda: et.lookup_(dst, A, I), steps, warmup, stream)
+    ok = bool(torch.equal(dst, data[I - 1]))  # bit copy check (torch gather as checker)
+    nbytes = B * (DIM * 4 * 2 + 8)
+    del data
+    return {"workload": "1 table 128 x 1e7 fp32, vector-index gather, B=65536",
+            "lookups_per_s": B / (ms * 1e-3), "kernel_ms": ms,
+            "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
+            "frac_of_hbm_peak": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_launch": nbytes, "bit_identical": ok}
+
+
+def zipf_indices(R, shape, alpha, gen, device):
+    """Bounded Zipf(alpha) ranks over 1..R by the continuous inverse CDF, mapped through
+    a seeded random permutation of the table."""
+    import torch
+
+    u = torch.rand(shape, generator=gen, device=device, dtype=torch.float64)
+    a1 = 1.0 - alpha
+    x = torch.floor(((float(R) ** a1 - 1.0) * u + 1.0) ** (1.0 / a1)).clamp_(1, R).long()
+    perm = torch.randperm(R, generator=gen, device=device)
+    return perm[x - 1] + 1
+
+
+def bench_config4(et, tables, tids, device, steps, warmup, batch):
+    """BASELINE configs[3]: the 26 tables, Zipf(1.05) indices, forward maplookup +
+    SparseEmbeddingUpdate fused Descent(0.1) over all tables (one SGD pipeline)."""
+    import torch
+    from embtab import _lib
+
+    stream = torch.cuda.current_stream(device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(4000)
+    idx = [zipf_indices(CRITEO_KAGGLE_ROWS[t], (batch, POOL), 1.05, gen, device) for t in tids]
+    ld = DIM * len(tables)
+    dst = torch.empty((batch, ld), dtype=torch.float32, device=device)
+    delta = torch.empty((batch, ld), dtype=torch.float32, device=device)
+    _lib.check(_lib.load().et_fill_uniform(_lib.ET_F32, delta.data_ptr(), delta.numel(), 4001, 0,
+                                           -1.0, 1.0, stream.cuda_stream))
+    strat = et.PreallocationStrategy(0)
+    opt = et.Descent(0.1)
+    grads = [et.SparseEmbeddingUpdate(A.lookup_type, delta[:, k * DIM:(k + 1) * DIM], i)
+             for k, (A, i) in enumerate(zip(tables, idx))]
+    indexers = [et.Indexer() for _ in tables]
+
+    def fwd():
+        et.maplookup_(strat, dst, tables, idx)
+
+    def upd():
+        et.update_(opt, tables, grads, indexers)
+
+    def step():
+        fwd()
+        upd()
+
+    fwd_ms = _timed(fwd, steps, warmup, stream)
+    upd_ms = _timed(upd, steps, warmup, stream)
+    step_ms = _timed(step, steps, warmup, stream)
+    U = sum(int(torch.unique(i).numel()) for i in idx)
+    occ = batch * POOL * len(tables)
+    upd_bytes = occ * 8 + batch * len(tables) * DIM * 4 + 2 * U * DIM * 4
+    hot = max(int(torch.bincount(i.view(-1)).max()) for i in idx)
+    return {"workload": "26 Criteo tables x 128 fp32, Zipf(1.05) pool-20 indices, B=65536: "
+                        "Preallocation forward + fused Descent(0.1) update of every table",
+            "lookups_per_s": occ / (step_ms * 1e-3), "step_ms": step_ms,
+            "forward_ms": fwd_ms, "update_ms": upd_ms,
+            "distinct_rows_U": U, "hottest_row_occurrences": hot,
+            "update_algorithmic_bytes": upd_bytes,
+            "update_achieved_GBs": upd_bytes / (upd_ms * 1e-3) / 1e9,
+            "update_delta_gather_bytes": occ * DIM * 4}
 
 
 def load_traffic():
@@ -263,6 +368,9 @@ def main():
     }
     if world > 1:
         result["lookup_only_ms"] = kernel_ms
+    if world == 1 and not args.no_extra:
+        result["config2_gather"] = bench_config2(et, L, device, 50, 5)
+        result["config4_zipf_update"] = bench_config4(et, tables, mine, device, 10, 2, B)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 16)
         threads = max(1, min(threads, os.cpu_count() or 1))
