@@ -117,31 +117,41 @@ class ShardedPreallocation:
         if self.world == 1:
             self.gathered[0].copy_(self.slab)
             return self.gathered
-        dist.all_gather_into_tensor(self.gathered.view(-1), self.slab.view(-1), group=self.group)
+        if dist.get_backend(self.group) == "gloo":  # CPU rehearsal: no all_gather_into_tensor
+            dist.all_gather(list(self.gathered.unbind(0)), self.slab, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self.gathered.view(-1), self.slab.view(-1),
+                                        group=self.group)
         return self.gathered
 
-    def assemble(self, dst: torch.Tensor):
-        """et_concat_slabs: every rank's slab rows into their dst rows."""
+    def assembly_launches(self):
+        """The et_concat_slabs launches that assemble the destination: a list of
+        ``(slab_row_shift, rows[rank], dst_row_off[rank])``.  With contiguous table
+        ranges per rank (plan_tables without sizes) this is one launch."""
+        launches = []
         max_runs = max(len(r) for r in self.runs)
-        L = _lib.load()
         for k in range(max_runs):
-            rows = (ctypes.c_int32 * self.world)()
-            offs = (ctypes.c_int64 * self.world)()
-            src_shift = [0] * self.world
+            per = {}
             for r in range(self.world):
                 if k < len(self.runs[r]):
                     srow, drow, n = self.runs[r][k]
-                    rows[r], offs[r], src_shift[r] = n, drow, srow
-            # slab rows of run k start at src_shift[r]; shift the slab base per rank by
-            # launching per distinct shift (usually a single launch with shift 0).
-            for shift in sorted(set(src_shift)):
-                rr = (ctypes.c_int32 * self.world)(*[rows[r] if src_shift[r] == shift else 0
-                                                     for r in range(self.world)])
-                base = self.gathered.data_ptr() + shift * self.gathered.element_size()
-                _lib.check(L.et_concat_slabs(
-                    _lib.et_dtype(dst), base, self.world, self.layout.slab_ld, self.batch,
-                    ctypes.addressof(rr), ctypes.addressof(offs), dst.data_ptr(), _ld(dst),
-                    _lib.stream_handle(dst.device)))
+                    rows, offs = per.setdefault(srow, ([0] * self.world, [0] * self.world))
+                    rows[r], offs[r] = n, drow
+            for shift in sorted(per):
+                launches.append((shift, per[shift][0], per[shift][1]))
+        return launches
+
+    def assemble(self, dst: torch.Tensor):
+        """et_concat_slabs: every rank's slab rows into their dst rows."""
+        L = _lib.load()
+        for shift, rows, offs in self.assembly_launches():
+            rr = (ctypes.c_int32 * self.world)(*rows)
+            oo = (ctypes.c_int64 * self.world)(*offs)
+            base = self.gathered.data_ptr() + shift * self.gathered.element_size()
+            _lib.check(L.et_concat_slabs(
+                _lib.et_dtype(dst), base, self.world, self.layout.slab_ld, self.batch,
+                ctypes.addressof(rr), ctypes.addressof(oo), dst.data_ptr(), _ld(dst),
+                _lib.stream_handle(dst.device)))
         return dst
 
     def __call__(self, local_tables, local_idx, dst: torch.Tensor):

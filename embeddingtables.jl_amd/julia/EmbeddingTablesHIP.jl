@@ -1,0 +1,261 @@
+# EmbeddingTablesHIP.jl — the Julia host layer of the MI355X engine.
+#
+# Plugs libembtab_hip.so (include/embtab.h) into darchr/EmbeddingTables.jl through the
+# package's own extension points (README.md:277-307, src/EmbeddingTables.jl:44-156):
+# a new `AbstractEmbeddingTable` subtype whose hot methods — `lookup!`,
+# `maplookup!(::PreallocationStrategy, …)` and `update!(::Descent, …)` — are `ccall`s
+# into the C ABI.  Everything else (lookup, maplookup, rrules, SparseEmbeddingUpdate,
+# Flux.Optimise.update!) is the reference's unchanged generic code.
+#
+# STATUS: written against the C ABI but NOT executed — this image has no Julia
+# toolchain (SURVEY.md §8c).  The Python ctypes layer (../embtab/) calls the identical
+# symbols with the identical arguments and is what the tests exercise; see
+# INTEGRATION.md for the one-to-one mapping.
+module EmbeddingTablesHIP
+
+using EmbeddingTables
+import EmbeddingTables: lookup!, maplookup!, update!, columnpointer, example, featuresize
+using EmbeddingTables: AbstractEmbeddingTable, Static, Dynamic, SparseEmbeddingUpdate,
+    PreallocationStrategy, AbstractIndexer, Indexer
+import Flux
+
+const libembtab = joinpath(@__DIR__, "..", "embtab", "libembtab_hip.so")
+const libhip = "libamdhip64.so"
+
+const ET_F32, ET_F16, ET_F64, ET_I32, ET_I64 = Cint(0), Cint(1), Cint(2), Cint(3), Cint(4)
+const ET_FLAG_NONTEMPORAL = UInt32(1)
+const ET_FLAG_SGD_UNFUSED = UInt32(8)
+const ET_FLAG_SGD_F64_ALPHA = UInt32(16)
+
+et_dtype(::Type{Float32}) = ET_F32
+et_dtype(::Type{Float16}) = ET_F16
+et_dtype(::Type{Float64}) = ET_F64
+et_dtype(::Type{Int32}) = ET_I32
+et_dtype(::Type{Int64}) = ET_I64
+
+struct EmbtabError <: Exception
+    status::Cint
+    msg::String
+end
+
+function check(rc::Cint)
+    if rc != 0
+        msg = unsafe_string(ccall((:et_last_error, libembtab), Cstring, ()))
+        throw(EmbtabError(rc, msg))
+    end
+    return nothing
+end
+
+# The stream every call is ordered on (NULL = the legacy default stream).
+const STREAM = Ref{Ptr{Cvoid}}(C_NULL)
+stream() = STREAM[]
+
+#####
+##### Device arrays (column-major, like Julia's own)
+#####
+
+mutable struct HipArray{T,N} <: AbstractArray{T,N}
+    ptr::Ptr{T}
+    dims::NTuple{N,Int}
+    function HipArray{T,N}(::UndefInitializer, dims::NTuple{N,Int}) where {T,N}
+        p = Ref{Ptr{Cvoid}}(C_NULL)
+        nbytes = max(prod(dims), 1) * sizeof(T)
+        ccall((:hipMalloc, libhip), Cint, (Ptr{Ptr{Cvoid}}, Csize_t), p, nbytes) == 0 ||
+            error("hipMalloc failed")
+        A = new{T,N}(Ptr{T}(p[]), dims)
+        finalizer(a -> ccall((:hipFree, libhip), Cint, (Ptr{Cvoid},), a.ptr), A)
+        return A
+    end
+end
+const HipVector{T} = HipArray{T,1}
+const HipMatrix{T} = HipArray{T,2}
+HipArray{T}(::UndefInitializer, dims::Integer...) where {T} =
+    HipArray{T,length(dims)}(undef, Int.(dims))
+Base.size(A::HipArray) = A.dims
+Base.pointer(A::HipArray) = A.ptr
+Base.similar(::HipArray, ::Type{T}, dims::Dims) where {T} = HipArray{T,length(dims)}(undef, dims)
+# Leading dimension in elements: HipArrays are dense.
+leading(A::HipMatrix) = size(A, 1)
+# Device memory is never dereferenced on the host: element access copies.
+function Base.getindex(A::HipArray{T}, i::Int) where {T}
+    r = Ref{T}()
+    ccall((:hipMemcpy, libhip), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Cint), r,
+          A.ptr + (i - 1) * sizeof(T), sizeof(T), 2)
+    return r[]
+end
+function Base.setindex!(A::HipArray{T}, v, i::Int) where {T}
+    r = Ref{T}(convert(T, v))
+    ccall((:hipMemcpy, libhip), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Cint),
+          A.ptr + (i - 1) * sizeof(T), r, sizeof(T), 1)
+    return v
+end
+Base.IndexStyle(::Type{<:HipArray}) = IndexLinear()
+
+#####
+##### The table type (AbstractEmbeddingTable contract, README.md:288-307)
+#####
+
+struct HipEmbedding{S,T} <: AbstractEmbeddingTable{S,T}
+    data::HipMatrix{T}
+end
+HipEmbedding(data::HipMatrix{T}) where {T} = HipEmbedding{Dynamic,T}(data)
+function HipEmbedding{Static{N}}(data::HipMatrix{T}) where {N,T}
+    N isa Int || throw(ArgumentError("Expected the type parameter for `Static{N}` to be an Int."))
+    N == size(data, 1) || throw(ArgumentError("Parameter `N` should match the number of rows."))
+    return HipEmbedding{Static{N},T}(data)
+end
+
+Base.size(A::HipEmbedding) = size(A.data)
+Base.getindex(A::HipEmbedding, i::Int) = A.data[i]
+Base.setindex!(A::HipEmbedding, v, i::Int) = (A.data[i] = v)
+# A DEVICE pointer: valid for the kernels, never for unsafe_load on the host.
+columnpointer(A::HipEmbedding{S,T}, i::Integer) where {S,T} =
+    A.data.ptr + (i - 1) * leading(A.data) * sizeof(T)
+example(A::HipEmbedding) = A.data
+
+# Preallocation gradients are row blocks of one big matrix: a view's leading dimension.
+_ptr_ld(A::HipMatrix) = (Ptr{Cvoid}(A.ptr), leading(A))
+function _ptr_ld(V::SubArray{T,2,<:HipMatrix{T}}) where {T}
+    P = parent(V)
+    r, c = first.(parentindices(V))
+    return Ptr{Cvoid}(P.ptr + ((c - 1) * leading(P) + (r - 1)) * sizeof(T)), leading(P)
+end
+
+#####
+##### lookup! — src/lookup.jl:42-43, :90-102, :167-182
+#####
+
+function lookup!(dst, A::HipEmbedding{S,T}, I::HipVector{Int}) where {S,T}
+    p, ld = _ptr_ld(dst)
+    check(ccall((:et_gather, libembtab), Cint,
+                (Cint, Ptr{Cvoid}, Int64, Int64, Int32, Ptr{Int64}, Int64, Ptr{Cvoid}, Int64,
+                 UInt32, Ptr{Cvoid}),
+                et_dtype(T), A.data.ptr, leading(A.data), size(A, 2), size(A, 1), I.ptr,
+                length(I), p, ld, ET_FLAG_NONTEMPORAL, stream()))
+    return dst
+end
+
+function lookup!(dst, A::HipEmbedding{S,T}, I::HipMatrix{Int}) where {S,T}
+    p, ld = _ptr_ld(dst)
+    check(ccall((:et_pooled_sum, libembtab), Cint,
+                (Cint, Ptr{Cvoid}, Int64, Int64, Int32, Ptr{Int64}, Int32, Int64, Int64,
+                 Ptr{Cvoid}, Int64, UInt32, Ptr{Cvoid}),
+                et_dtype(T), A.data.ptr, leading(A.data), size(A, 2), size(A, 1), I.ptr,
+                size(I, 1), size(I, 1), size(I, 2), p, ld, ET_FLAG_NONTEMPORAL, stream()))
+    return dst
+end
+
+#####
+##### maplookup!(::PreallocationStrategy) — src/lookup.jl:316-371, ONE launch
+#####
+
+struct LookupDesc
+    table::Ptr{Cvoid}
+    ld_table::Int64
+    nrows::Int64
+    dim::Int32
+    pool::Int32
+    idx::Ptr{Int64}
+    ld_idx::Int64
+    dst_row_off::Int64
+end
+
+function maplookup!(strategy::PreallocationStrategy, dst::HipMatrix{T},
+                    x::Vector{<:HipEmbedding{<:Any,T}}, I0; kw...) where {T}
+    I = EmbeddingTables.colwrap(I0)
+    descs = Vector{LookupDesc}(undef, length(x))
+    off = strategy.prependrows
+    for (t, (A, i)) in enumerate(zip(x, I))
+        pool = ndims(i) == 1 ? 1 : size(i, 1)
+        descs[t] = LookupDesc(A.data.ptr, leading(A.data), size(A, 2), size(A, 1), pool,
+                              pointer(i), pool, off)
+        off += size(A, 1)
+    end
+    check(ccall((:et_maplookup_prealloc, libembtab), Cint,
+                (Cint, Ptr{LookupDesc}, Int32, Int64, Ptr{Cvoid}, Int64, UInt32, Ptr{Cvoid}),
+                et_dtype(T), descs, length(descs), EmbeddingTables._batchsize(I), dst.ptr,
+                leading(dst), ET_FLAG_NONTEMPORAL, stream()))
+    return dst
+end
+
+#####
+##### update! — src/sparseupdate.jl:160-178 (single) and :199-238 (multi-table)
+#####
+
+struct UpdateDesc
+    table::Ptr{Cvoid}
+    ld_table::Int64
+    nrows::Int64
+    dim::Int32
+    pool::Int32
+    delta::Ptr{Cvoid}
+    ld_delta::Int64
+    idx::Ptr{Int64}
+    ld_idx::Int64
+    batch::Int64
+end
+
+function _update_desc(A::HipEmbedding{S,Float32}, g::SparseEmbeddingUpdate) where {S}
+    dp, dld = _ptr_ld(g.delta)
+    I = g.indices
+    pool = ndims(I) == 1 ? 1 : size(I, 1)
+    return UpdateDesc(A.data.ptr, leading(A.data), size(A, 2), size(A, 1), pool, dp, dld,
+                      pointer(I), pool, size(I, ndims(I)))
+end
+
+# The reference picks its fused `muladd` kernel for Static tables of <= 512 bytes per
+# column (src/sparseupdate.jl:131-154), the generic `x - alpha*y` path otherwise.
+_fused(::HipEmbedding{Static{N},T}) where {N,T} = N * sizeof(T) <= 512
+_fused(::HipEmbedding) = false
+
+const WORKSPACE = Ref{Any}(nothing)
+function _workspace(nbytes)
+    ws = WORKSPACE[]
+    if ws === nothing || length(ws) < nbytes
+        ws = HipArray{UInt8}(undef, nbytes)
+        WORKSPACE[] = ws
+    end
+    return ws
+end
+
+function _sparse_sgd(descs::Vector{UpdateDesc}, eta::Float64, flags::UInt32)
+    nb = Ref{Int64}(0)
+    check(ccall((:et_sgd_workspace_size, libembtab), Cint, (Ptr{UpdateDesc}, Int32, Ref{Int64}),
+                descs, length(descs), nb))
+    ws = _workspace(nb[])
+    check(ccall((:et_sparse_sgd, libembtab), Cint,
+                (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                ET_F32, descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
+end
+
+function update!(opt::Flux.Descent, table::HipEmbedding{S,Float32}, grad::SparseEmbeddingUpdate,
+                 indexer = Indexer(), ::Val{Nontemporal} = Val(true), args...) where {S,Nontemporal}
+    flags = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
+            (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED)
+    # convert(eltype(table), opt.eta) happens inside the fp32 kernel
+    _sparse_sgd([_update_desc(table, grad)], Float64(opt.eta), flags)
+    return nothing
+end
+
+function update!(opt::Flux.Descent, tables::AbstractVector{<:HipEmbedding},
+                 grads::AbstractVector{<:SparseEmbeddingUpdate},
+                 indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
+                 telemetry_cb = Returns(nothing), kw...) where {Nontemporal}
+    telemetry_cb()
+    nt = Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)
+    for fused in (true, false)
+        sel = [i for i in eachindex(tables) if _fused(tables[i]) == fused]
+        isempty(sel) && continue
+        # the multi-table generic path sees opt.eta as Float64 (src/sparseupdate.jl:232)
+        flags = nt | (fused ? UInt32(0) : ET_FLAG_SGD_UNFUSED | ET_FLAG_SGD_F64_ALPHA)
+        for chunk in Iterators.partition(sel, 32)
+            _sparse_sgd([_update_desc(tables[i], grads[i]) for i in chunk], Float64(opt.eta),
+                        flags)
+        end
+    end
+    return nothing
+end
+
+export HipEmbedding, HipArray, HipVector, HipMatrix, EmbtabError
+
+end # module

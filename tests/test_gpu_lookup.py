@@ -220,3 +220,21 @@ def test_concat_slabs():
     got = host(dst)
     for r in range(nranks):
         assert np.array_equal(got[:, offs[r]:offs[r] + rows[r]], slabs[r][:, :rows[r]])
+
+
+def test_sharded_prealloc_single_rank(oracle):
+    """embtab.sharding end to end on one GPU (world 1): local fused lookup into the
+    slab, exchange, et_concat_slabs assembly — equals the unsharded Preallocation."""
+    from embtab.sharding import ShardLayout, ShardedPreallocation, plan_tables
+
+    rng = np.random.default_rng(8)
+    dims = [128] * 6
+    rows = [300, 5000, 20, 800, 64, 1000]
+    hs = [rng.random((r, d), dtype=np.float32) for r, d in zip(rows, dims)]
+    hidx = [rng.integers(1, r + 1, (256, 20)) for r in rows]
+    layout = ShardLayout(dims, 4, plan_tables(6, 1))
+    sp = ShardedPreallocation(layout, 0, 1, 256, torch.float32, DEV)
+    dst = torch.zeros((256, layout.ld), dtype=torch.float32, device=DEV)
+    sp([table(h) for h in hs], [dev(i) for i in hidx], dst)
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=4)
+    assert bits_equal(host(dst)[:, 4:], ref[:, 4:])
