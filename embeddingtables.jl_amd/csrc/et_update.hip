@@ -133,35 +133,52 @@ __device__ __forceinline__ float sgd_apply(float w, float acc, float eta32, doub
     return (float)__dsub_rn((double)w, __dmul_rn(eta64, (double)acc));
 }
 
-// Sum delta columns of occurrences [s0, s1) of the sorted order into acc (one lane
-// group, feature vector of D fp32 as 16-B vectors).  Values are occurrence ids;
-// bag = (o - occ_off[t]) / pool_t.
+// Value of lane (base + g) for group g (base wave-uniform): readlane + select for <= 4
+// groups per wave, ds_bpermute otherwise.
+template <int GPW>
+__device__ __forceinline__ uint32_t group_pick(uint32_t v, int base, int g) {
+    if constexpr (GPW <= 4) {
+        uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, base);
+#pragma unroll
+        for (int gg = 1; gg < GPW; ++gg) {
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)v, base + gg);
+            r = g == gg ? t : r;
+        }
+        return r;
+    } else {
+        return (uint32_t)__shfl((int)v, base + g, 64);
+    }
+}
+
+// Sum the delta columns of sorted occurrences [s0, s1) into acc, in order (one lane
+// group; a row of D fp32 is LPR lanes x NV 16-B vectors).  The group reads LPR
+// occurrence ids at once (coalesced), turns them into bag numbers, broadcasts them
+// lane by lane and keeps U column loads in flight.  The groups of a wave walk chunks
+// of different lengths, so loop counters are NOT wave-uniform here: the broadcast is a
+// ds_bpermute (per-lane source index), never a readlane.
 template <int D, int U>
-__device__ __forceinline__ void chunk_sum(const UpdatePack& p, int t,
-                                          const uint32_t* __restrict__ vals, uint32_t s0,
-                                          uint32_t s1, int sub, int gbase, float (&acc)[D / 4 / (D / 4 < 64 ? D / 4 : 64)][4]) {
+__device__ __forceinline__ void occ_sum(const float* __restrict__ delta, uint32_t ld_delta,
+                                        uint32_t occ_off, uint32_t pool,
+                                        const uint32_t* __restrict__ vals, uint32_t s0,
+                                        uint32_t s1, int g, int sub,
+                                        float (&acc)[(D / 4 < 64 ? 1 : D / 4 / 64)][4]) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
-    const et_update_desc& d = p.d[t];
-    const float* delta = reinterpret_cast<const float*>(d.delta);
-    const uint64_t ldd = (uint64_t)d.ld_delta;
-    const uint32_t ooff = p.occ_off[t], pool = (uint32_t)d.pool;
     for (uint32_t c0 = s0; c0 < s1; c0 += LPR) {
         const int cnt = (int)(s1 - c0 < (uint32_t)LPR ? s1 - c0 : (uint32_t)LPR);
         const uint32_t myo = vals[c0 + (uint32_t)(sub < cnt ? sub : cnt - 1)];
-        const uint32_t mybag = (myo - ooff) / pool;
-        int i0 = 0;
-        for (; i0 < cnt; i0 += U) {
+        const int mybag = (int)((myo - occ_off) / pool);
+        for (int i0 = 0; i0 < cnt; i0 += U) {
             const int m = cnt - i0 < U ? cnt - i0 : U;
-            u32x4 buf[U][NV];
             uint64_t off[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int slot = i0 + (u < m ? u : m - 1);
-                const uint32_t bag = (uint32_t)__shfl((int)mybag, gbase + slot, 64);
-                off[u] = (uint64_t)bag * ldd;
+                const uint32_t bag = (uint32_t)__shfl(mybag, g * LPR + slot, 64);
+                off[u] = (uint64_t)bag * ld_delta;
             }
+            u32x4 buf[U][NV];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const u32x4* src = reinterpret_cast<const u32x4*>(delta + off[u]) + sub;
@@ -186,6 +203,31 @@ __device__ __forceinline__ void chunk_sum(const UpdatePack& p, int t,
 }
 
 template <int D, int MODE, bool NT>
+__device__ __forceinline__ void apply_row(float* __restrict__ w, const u32x4 (&x)[(D / 4 < 64 ? 1 : D / 4 / 64)],
+                                          const float (&acc)[(D / 4 < 64 ? 1 : D / 4 / 64)][4],
+                                          int sub, float eta32, double eta64) {
+    constexpr int VPR = D / 4;
+    constexpr int LPR = VPR < 64 ? VPR : 64;
+    constexpr int NV = VPR / LPR;
+    u32x4* wp = reinterpret_cast<u32x4*>(w) + sub;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        u32x4 y;
+        y.x = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x[v].x), acc[v][0], eta32, eta64));
+        y.y = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x[v].y), acc[v][1], eta32, eta64));
+        y.z = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x[v].z), acc[v][2], eta32, eta64));
+        y.w = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x[v].w), acc[v][3], eta32, eta64));
+        store16<NT>(wp + v * LPR, y);
+    }
+}
+
+// Chunk pass.  Each wave takes 64 chunks spaced `nwaves` apart (so the consecutive
+// chunks of a hot segment land on different waves), loads their metadata once (one
+// chunk per lane), and its lane groups walk them, reading a chunk's fields from the
+// metadata lanes with v_readlane.  Single-chunk segments read the table column before
+// the gradient sum (so the read overlaps the delta gathers) and apply the update;
+// chunks of longer segments store a partial row.
+template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chunks(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const uint32_t* __restrict__ seg_start,
@@ -198,51 +240,67 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
     constexpr int NV = VPR / LPR;
     constexpr int GPW = 64 / LPR;
     constexpr int U = NV >= 8 ? 1 : 8 / NV;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane / LPR, sub = lane % LPR;
     const uint32_t C = counters[kCntC];
-    const uint32_t groups = gridDim.x * 4 * GPW;
-    for (uint32_t c = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GPW + g; c < C; c += groups) {
+    const uint32_t nwaves = gridDim.x * 4u;
+    const uint32_t wid = blockIdx.x * 4u + wave;
+    for (uint32_t it = 0; (uint64_t)it * 64u * nwaves + wid < C; ++it) {
+        // metadata of chunks (it*64 + l) * nwaves + wid, one per lane l
+        const uint64_t cl = ((uint64_t)it * 64u + lane) * nwaves + wid;
+        const bool valid = cl < C;
+        const uint32_t c = valid ? (uint32_t)cl : C - 1;
         const uint32_t u = chunk_seg[c];
-        const uint32_t pidx = c - chunk_start[u];
-        const uint32_t nchunks = chunk_start[u + 1] - chunk_start[u];
-        const uint32_t seg0 = seg_start[u], seg1 = seg_start[u + 1];
-        const uint32_t key = keys[seg0];
-        if (key == sent) continue;  // out-of-range indices: skipped
-        const int t = table_of_key(pack, ntables, key);
-        if (pack.d[t].dim != D) continue;  // another dim group's launch
-        const uint32_t s0 = seg0 + pidx * chunk;
-        const uint32_t s1 = s0 + chunk < seg1 ? s0 + chunk : seg1;
-        float acc[NV][4];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
-        chunk_sum<D, U>(pack, t, vals, s0, s1, sub, g * LPR, acc);
-        if (nchunks == 1) {
+        const uint32_t cs = chunk_start[u], ce = chunk_start[u + 1];
+        const uint32_t ss = seg_start[u], se = seg_start[u + 1];
+        const uint32_t key = keys[ss];
+        const uint32_t ps = partial_start[u];
+        const uint32_t p = c - cs;
+        const uint32_t m_s0 = ss + p * chunk;
+        const uint32_t m_s1 = m_s0 + chunk < se ? m_s0 + chunk : se;
+        const uint32_t m_dst = (ce - cs == 1) ? 0xffffffffu : ps + p;
+        const uint32_t m_key = valid ? key : sent;
+        const uint64_t left = ((uint64_t)C - wid + nwaves - 1) / nwaves - (uint64_t)it * 64u;
+        const uint32_t nq = left < 64u ? (uint32_t)left : 64u;
+        for (uint32_t qq = 0; qq < nq; qq += GPW) {
+            const uint32_t kkey = group_pick<GPW>(m_key, (int)qq, g);
+            const uint32_t s0 = group_pick<GPW>(m_s0, (int)qq, g);
+            const uint32_t s1 = group_pick<GPW>(m_s1, (int)qq, g);
+            const uint32_t dsl = group_pick<GPW>(m_dst, (int)qq, g);
+            if (qq + g >= nq || kkey == sent) continue;  // past the end / bad indices
+            const int t = table_of_key(pack, ntables, kkey);
             const et_update_desc& d = pack.d[t];
+            if (d.dim != D) continue;  // another dim group's launch
             float* w = reinterpret_cast<float*>(d.table) +
-                       (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table;
-            u32x4* wp = reinterpret_cast<u32x4*>(w) + sub;
+                       (uint64_t)(kkey - pack.row_off[t]) * (uint64_t)d.ld_table;
+            u32x4 x[NV];
+            if (dsl == 0xffffffffu) {
+                const u32x4* wp = reinterpret_cast<const u32x4*>(w) + sub;
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const u32x4 x = wp[v * LPR];
-                u32x4 y;
-                y.x = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.x), acc[v][0], eta32, eta64));
-                y.y = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.y), acc[v][1], eta32, eta64));
-                y.z = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.z), acc[v][2], eta32, eta64));
-                y.w = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.w), acc[v][3], eta32, eta64));
-                store16<NT>(wp + v * LPR, y);
+                for (int v = 0; v < NV; ++v) x[v] = wp[v * LPR];
             }
-        } else {
-            float* pr = partials + (uint64_t)(partial_start[u] + pidx) * (uint64_t)pdim;
-            u32x4* pp = reinterpret_cast<u32x4*>(pr) + sub;
+            float acc[NV][4];
 #pragma unroll
-            for (int v = 0; v < NV; ++v)
-                pp[v * LPR] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
-                                    __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
+            for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
+            occ_sum<D, U>(reinterpret_cast<const float*>(d.delta), (uint32_t)d.ld_delta,
+                          pack.occ_off[t], (uint32_t)d.pool, vals, s0, s1, g, sub, acc);
+            if (dsl == 0xffffffffu) {
+                apply_row<D, MODE, NT>(w, x, acc, sub, eta32, eta64);
+            } else {
+                u32x4* pp = reinterpret_cast<u32x4*>(partials + (uint64_t)dsl * pdim) + sub;
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    pp[v * LPR] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
+                                        __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
+            }
         }
     }
 }
 
+// Combine pass: every multi-chunk segment is reduced by a whole workgroup.  Its
+// partial rows are split into NG = 4*GPW contiguous ranges in chunk order; group G sums
+// range G sequentially (U rows in flight), the NG sums are added in group order
+// through LDS and group 0 applies the update.  Fixed partition => deterministic.
 template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_combine(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
@@ -253,44 +311,86 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
     constexpr int GPW = 64 / LPR;
+    constexpr int NG = 4 * GPW;
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
+    __shared__ uint32_t list[256];
+    __shared__ uint32_t nlist;
+    __shared__ u32x4 red[NG][LPR * NV];
     const int lane = threadIdx.x & 63;
-    const int g = lane / LPR, sub = lane % LPR;
+    const int G = threadIdx.x / LPR, sub = lane % LPR;
     const uint32_t Useg = counters[kCntU];
-    const uint32_t groups = gridDim.x * 4 * GPW;
-    for (uint32_t u = (blockIdx.x * 4 + (threadIdx.x >> 6)) * GPW + g; u < Useg; u += groups) {
-        const uint32_t p0 = partial_start[u], p1 = partial_start[u + 1];
-        if (p1 == p0) continue;  // single-chunk segment: already applied
-        const uint32_t key = keys[seg_start[u]];
-        if (key == sent) continue;
-        const int t = table_of_key(pack, ntables, key);
-        if (pack.d[t].dim != D) continue;
-        float acc[NV][4];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
-        for (uint32_t q = p0; q < p1; ++q) {
-            const u32x4* pp = reinterpret_cast<const u32x4*>(partials + (uint64_t)q * pdim) + sub;
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const u32x4 b = pp[v * LPR];
-                acc[v][0] = acc[v][0] + __uint_as_float(b.x);
-                acc[v][1] = acc[v][1] + __uint_as_float(b.y);
-                acc[v][2] = acc[v][2] + __uint_as_float(b.z);
-                acc[v][3] = acc[v][3] + __uint_as_float(b.w);
-            }
+    for (uint32_t base = blockIdx.x * 256u; base < Useg; base += gridDim.x * 256u) {
+        if (threadIdx.x == 0) nlist = 0;
+        __syncthreads();
+        const uint32_t u = base + threadIdx.x;
+        if (u < Useg && partial_start[u + 1] > partial_start[u]) {
+            const uint32_t key = keys[seg_start[u]];
+            if (key != sent && pack.d[table_of_key(pack, ntables, key)].dim == D)
+                list[atomicAdd(&nlist, 1u)] = u;
         }
-        const et_update_desc& d = pack.d[t];
-        float* w = reinterpret_cast<float*>(d.table) +
-                   (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table;
-        u32x4* wp = reinterpret_cast<u32x4*>(w) + sub;
+        __syncthreads();
+        const uint32_t nl = nlist;
+        for (uint32_t k = 0; k < nl; ++k) {
+            const uint32_t seg = list[k];
+            const uint32_t p0 = partial_start[seg], np = partial_start[seg + 1] - p0;
+            const uint32_t a = p0 + (uint32_t)((uint64_t)np * G / NG);
+            const uint32_t b = p0 + (uint32_t)((uint64_t)np * (G + 1) / NG);
+            float acc[NV][4];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const u32x4 x = wp[v * LPR];
-            u32x4 y;
-            y.x = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.x), acc[v][0], eta32, eta64));
-            y.y = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.y), acc[v][1], eta32, eta64));
-            y.z = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.z), acc[v][2], eta32, eta64));
-            y.w = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x.w), acc[v][3], eta32, eta64));
-            store16<NT>(wp + v * LPR, y);
+            for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
+            for (uint32_t q0 = a; q0 < b; q0 += U) {
+                u32x4 buf[U][NV];
+#pragma unroll
+                for (int uu = 0; uu < U; ++uu) {
+                    const uint32_t q = q0 + uu < b ? q0 + uu : b - 1;
+                    const u32x4* pp = reinterpret_cast<const u32x4*>(partials + (uint64_t)q * pdim) + sub;
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) buf[uu][v] = pp[v * LPR];
+                }
+#pragma unroll
+                for (int uu = 0; uu < U; ++uu) {
+                    if (q0 + uu < b) {
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) {
+                            acc[v][0] = acc[v][0] + __uint_as_float(buf[uu][v].x);
+                            acc[v][1] = acc[v][1] + __uint_as_float(buf[uu][v].y);
+                            acc[v][2] = acc[v][2] + __uint_as_float(buf[uu][v].z);
+                            acc[v][3] = acc[v][3] + __uint_as_float(buf[uu][v].w);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                red[G][v * LPR + sub] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
+                                              __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
+            __syncthreads();
+            if (G == 0) {
+                float tot[NV][4];
+#pragma unroll
+                for (int v = 0; v < NV; ++v) tot[v][0] = tot[v][1] = tot[v][2] = tot[v][3] = 0.0f;
+                for (int gg = 0; gg < NG; ++gg) {
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        const u32x4 r = red[gg][v * LPR + sub];
+                        tot[v][0] = tot[v][0] + __uint_as_float(r.x);
+                        tot[v][1] = tot[v][1] + __uint_as_float(r.y);
+                        tot[v][2] = tot[v][2] + __uint_as_float(r.z);
+                        tot[v][3] = tot[v][3] + __uint_as_float(r.w);
+                    }
+                }
+                const uint32_t key = keys[seg_start[seg]];
+                const int t = table_of_key(pack, ntables, key);
+                const et_update_desc& d = pack.d[t];
+                float* w = reinterpret_cast<float*>(d.table) +
+                           (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table;
+                u32x4 x[NV];
+                const u32x4* wp = reinterpret_cast<const u32x4*>(w) + sub;
+#pragma unroll
+                for (int v = 0; v < NV; ++v) x[v] = wp[v * LPR];
+                apply_row<D, MODE, NT>(w, x, tot, sub, eta32, eta64);
+            }
+            __syncthreads();
         }
     }
 }
