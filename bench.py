@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--no-check", action="store_true", help="skip the CPU/GPU bit comparison")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the config-2 (gather) and config-4 (Zipf + SGD) measurements")
+    p.add_argument("--subset", choices=["all", "heavy", "light"], default="all",
+                   help="calibration only: tables above / below 4 MiB")
     p.add_argument("--rows", type=int, default=0,
                    help="calibration only: give every table this many rows (0 = Criteo)")
     return p.parse_args()
@@ -266,6 +268,9 @@ def main():
         dist.init_process_group("nccl", device_id=device)
     L = _lib.load()
     B = args.batch
+    if args.subset != "all":
+        keep = [r for r in CRITEO_KAGGLE_ROWS if (r * DIM * 4 > (4 << 20)) == (args.subset == "heavy")]
+        CRITEO_KAGGLE_ROWS[:] = keep
     T = len(CRITEO_KAGGLE_ROWS)
     dims = [DIM] * T
     assignment = plan_tables(T, world)

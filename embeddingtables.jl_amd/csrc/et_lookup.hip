@@ -80,10 +80,14 @@ __device__ __forceinline__ long long group_bcast(long long v, int i, int g) {
 
 // The first (up to) LPR indices of a bag, one per lane of the group; lanes past the
 // end re-read the last one so that no lane is masked off.
-template <int LPR>
+template <int LPR, bool NTI = false>
 __device__ __forceinline__ long long load_idx_chunk(const int64_t* __restrict__ ip, int cnt,
                                                     int sub) {
-    return (long long)ip[sub < cnt ? sub : cnt - 1];
+    const int64_t* p = ip + (sub < cnt ? sub : cnt - 1);
+    if constexpr (NTI)
+        return (long long)__builtin_nontemporal_load(p);
+    else
+        return (long long)*p;
 }
 
 // Issue UU row loads of one bag (slots i0 .. i0+UU-1 of the current index chunk, all
@@ -204,7 +208,7 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_
 
 // `rounds` bags of one table per lane group, the next bag's first index chunk loaded
 // while the current bag's rows are in flight.
-template <typename T, typename A, int D, int U, bool NT, bool NTL>
+template <typename T, typename A, int D, int U, bool NT, bool NTL, bool NTI = false>
 __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
                                          T* __restrict__ dst, int64_t ld_dst, int64_t chunk,
                                          int rounds) {
@@ -217,15 +221,15 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
     const int cnt0 = pool < G::LPR ? pool : G::LPR;
     const uint32_t ldt = (uint32_t)d.ld_table, nr = (uint32_t)d.nrows;
     int64_t bag = chunk * per_round * rounds + wave * G::GPW + g;
-    long long my_next = load_idx_chunk<G::LPR>(
+    long long my_next = load_idx_chunk<G::LPR, NTI>(
         d.idx + (bag < batch ? bag : batch - 1) * d.ld_idx, cnt0, sub);
     for (int r = 0; r < rounds; ++r) {
         if (bag >= batch) break;
         const long long my = my_next;
         const int64_t nbag = bag + per_round;
         if (r + 1 < rounds)
-            my_next = load_idx_chunk<G::LPR>(d.idx + (nbag < batch ? nbag : batch - 1) * d.ld_idx,
-                                             cnt0, sub);
+            my_next = load_idx_chunk<G::LPR, NTI>(
+                d.idx + (nbag < batch ? nbag : batch - 1) * d.ld_idx, cnt0, sub);
         bag_sum_vec<T, A, D, U, NT, NTL>(table, ldt, nr, d.idx + bag * d.ld_idx, pool, my,
                                          dst + bag * ld_dst + d.dst_row_off, g, sub);
         bag = nbag;
@@ -260,7 +264,7 @@ struct StripeMap {
     uint32_t ntload_mask;  // bit t: non-temporal row loads for table t
 };
 
-template <typename T, typename A, int D, int U, bool NT>
+template <typename T, typename A, int D, int U, bool NT, bool NTI = false>
 __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, StripeMap sm,
                                                             int ntables, int64_t batch,
                                                             T* __restrict__ dst, int64_t ld_dst,
@@ -275,9 +279,9 @@ __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, Str
     const int64_t chunk = (int64_t)(e >> 8) * stripe_chunks + j;
     if (j >= stripe_chunks || chunk >= nchunks) return;
     if ((sm.ntload_mask >> t) & 1u)
-        run_bags<T, A, D, U, NT, true>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+        run_bags<T, A, D, U, NT, true, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
     else
-        run_bags<T, A, D, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+        run_bags<T, A, D, U, NT, false, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
 }
 
 // Non-reducing gather (bit copy) of RB-byte rows: each group moves U rows at once.
@@ -413,7 +417,12 @@ inline int rounds_for(int64_t batch, int64_t bags_per_round, int ntables) {
 // Scheduling knobs (read once; for experiments — the defaults are the tuned choice).
 struct LookupTuning {
     int striped = 1;               // ET_SCHED=linear disables the XCD stripe schedule
-    int ntload = 0;                // ET_NTLOAD=1: non-temporal row loads of heavy tables
+    // Tables larger than the 256 MiB Infinity Cache cannot stay cache resident: their
+    // rows are loaded non-temporally so they do not evict the light tables from L2
+    // (measured -5% on the Criteo mix; nt on the cache-resident mid-size tables hurts).
+    int ntload = 1;                          // ET_NTLOAD=0 disables
+    int64_t ntload_bytes = 256ll << 20;      // ET_NTLOAD_BYTES
+    int ntidx = 0;                           // ET_NTIDX=1: non-temporal index loads
     int64_t light_bytes = 4 << 20; // tables up to one XCD L2 (4 MiB) are "light"
     int rows_in_flight = 0;        // ET_U=4|8|16: rows per group in flight (fp32 D=128)
 };
@@ -423,6 +432,8 @@ inline const LookupTuning& tuning() {
         LookupTuning v;
         if (const char* e = getenv("ET_SCHED")) v.striped = strcmp(e, "linear") != 0;
         if (const char* e = getenv("ET_NTLOAD")) v.ntload = atoi(e);
+        if (const char* e = getenv("ET_NTLOAD_BYTES")) v.ntload_bytes = atoll(e);
+        if (const char* e = getenv("ET_NTIDX")) v.ntidx = atoi(e);
         if (const char* e = getenv("ET_LIGHT_BYTES")) v.light_bytes = atoll(e);
         if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
         return v;
@@ -442,7 +453,7 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
         bytes[t] = pack.d[t].nrows * pack.d[t].ld_table * es;
         if (bytes[t] > tu.light_bytes) {
             heavy[nh++] = t;
-            if (tu.ntload) sm.ntload_mask |= 1u << t;
+            if (tu.ntload && bytes[t] > tu.ntload_bytes) sm.ntload_mask |= 1u << t;
         } else {
             light[nl++] = t;
         }
@@ -498,9 +509,14 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
         const int64_t grid = (int64_t)kXcds * n * stripe_chunks;
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
-        hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT>), dim3((unsigned)grid),
-                           dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst), ld_dst,
-                           rounds, stripe_chunks, nchunks);
+        if (tuning().ntidx && D == 128 && __is_same(T, float))
+            hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT, true>), dim3((unsigned)grid),
+                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               ld_dst, rounds, stripe_chunks, nchunks);
+        else
+            hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT>), dim3((unsigned)grid),
+                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               ld_dst, rounds, stripe_chunks, nchunks);
         ET_LAUNCH_CHECK("k_pooled_vec_striped");
         return ET_OK;
     }
