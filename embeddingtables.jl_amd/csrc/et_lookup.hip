@@ -406,11 +406,14 @@ inline bool gather_rb_ok(int64_t rb) {
 }
 
 // Bags per workgroup round for the vector path.
+int max_rounds();
+
 inline int rounds_for(int64_t batch, int64_t bags_per_round, int ntables) {
     // Aim for >= ~8 workgroups per CU (2048) before making workgroups longer.
     int64_t blocks1 = (batch + bags_per_round - 1) / bags_per_round * ntables;
     int rounds = 1;
-    while (rounds < 8 && blocks1 / (rounds * 2) >= 4096) rounds *= 2;
+    const int mr = max_rounds();
+    while (rounds < mr && blocks1 / (rounds * 2) >= 4096) rounds *= 2;
     return rounds;
 }
 
@@ -423,6 +426,7 @@ struct LookupTuning {
     int ntload = 1;                          // ET_NTLOAD=0 disables
     int64_t ntload_bytes = 256ll << 20;      // ET_NTLOAD_BYTES
     int ntidx = 0;                           // ET_NTIDX=1: non-temporal index loads
+    int max_rounds = 8;                      // ET_ROUNDS: max bag rounds per workgroup
     int64_t light_bytes = 4 << 20; // tables up to one XCD L2 (4 MiB) are "light"
     int rows_in_flight = 0;        // ET_U=4|8|16: rows per group in flight (fp32 D=128)
 };
@@ -434,12 +438,15 @@ inline const LookupTuning& tuning() {
         if (const char* e = getenv("ET_NTLOAD")) v.ntload = atoi(e);
         if (const char* e = getenv("ET_NTLOAD_BYTES")) v.ntload_bytes = atoll(e);
         if (const char* e = getenv("ET_NTIDX")) v.ntidx = atoi(e);
+        if (const char* e = getenv("ET_ROUNDS")) v.max_rounds = atoi(e) > 0 ? atoi(e) : 1;
         if (const char* e = getenv("ET_LIGHT_BYTES")) v.light_bytes = atoll(e);
         if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
         return v;
     }();
     return t;
 }
+
+int max_rounds() { return tuning().max_rounds; }
 
 // Stripe assignment: heavy tables -> stripe x on XCD x; light tables' stripes laid out
 // table after table (alternating large and small tables) and cut into kXcds equal runs.
