@@ -39,7 +39,7 @@ struct UpdatePack {
 };
 
 // Counters in the workspace.
-enum { kCntU = 0, kCntC = 1, kCntSlots = 16 };
+enum { kCntU = 0, kCntC = 1, kCntM = 2, kCntSlots = 16 };
 
 __device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, uint32_t key) {
     int t = 0;
@@ -95,11 +95,14 @@ __global__ __launch_bounds__(256) void k_seg_start(const uint32_t* __restrict__ 
     }
 }
 
-// nchunks per segment (0 beyond U), multi-chunk partial slots per segment.
+// nchunks per segment (0 beyond U), multi-chunk partial slots per segment; multi-chunk
+// segments are also appended to `mlist` (order irrelevant: each is reduced by exactly
+// one workgroup in a fixed order, so results do not depend on it).
 __global__ __launch_bounds__(256) void k_seg_chunks(const uint32_t* __restrict__ seg_start,
-                                                    int64_t n, const uint32_t* __restrict__ counters,
+                                                    int64_t n, uint32_t* __restrict__ counters,
                                                     uint32_t chunk, uint32_t* __restrict__ nch,
-                                                    uint32_t* __restrict__ multi) {
+                                                    uint32_t* __restrict__ multi,
+                                                    uint32_t* __restrict__ mlist) {
     const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (u > n) return;
     const uint32_t U = counters[kCntU];
@@ -110,6 +113,7 @@ __global__ __launch_bounds__(256) void k_seg_chunks(const uint32_t* __restrict__
     }
     nch[u] = c;
     multi[u] = c > 1 ? c : 0u;
+    if (c > 1) mlist[atomicAdd(&counters[kCntM], 1u)] = (uint32_t)u;
 }
 
 __global__ __launch_bounds__(256) void k_chunk_seg(const uint32_t* __restrict__ chunk_start,
@@ -297,7 +301,8 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
     }
 }
 
-// Combine pass: every multi-chunk segment is reduced by a whole workgroup.  Its
+// Combine pass: every multi-chunk segment (from the appended list, one per workgroup
+// at a time) is reduced by a whole workgroup.  Its
 // partial rows are split into NG = 4*GPW contiguous ranges in chunk order; group G sums
 // range G sequentially (U rows in flight), the NG sums are added in group order
 // through LDS and group 0 applies the update.  Fixed partition => deterministic.
@@ -305,33 +310,26 @@ template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_combine(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
-    const uint32_t* __restrict__ counters, const float* __restrict__ partials, int pdim,
-    uint32_t sent, float eta32, double eta64) {
+    const uint32_t* __restrict__ counters, const uint32_t* __restrict__ mlist,
+    const float* __restrict__ partials, int pdim, uint32_t sent, float eta32, double eta64) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
     constexpr int GPW = 64 / LPR;
     constexpr int NG = 4 * GPW;
     constexpr int U = NV >= 8 ? 1 : 8 / NV;
-    __shared__ uint32_t list[256];
-    __shared__ uint32_t nlist;
     __shared__ u32x4 red[NG][LPR * NV];
     const int lane = threadIdx.x & 63;
     const int G = threadIdx.x / LPR, sub = lane % LPR;
-    const uint32_t Useg = counters[kCntU];
-    for (uint32_t base = blockIdx.x * 256u; base < Useg; base += gridDim.x * 256u) {
-        if (threadIdx.x == 0) nlist = 0;
-        __syncthreads();
-        const uint32_t u = base + threadIdx.x;
-        if (u < Useg && partial_start[u + 1] > partial_start[u]) {
-            const uint32_t key = keys[seg_start[u]];
-            if (key != sent && pack.d[table_of_key(pack, ntables, key)].dim == D)
-                list[atomicAdd(&nlist, 1u)] = u;
-        }
-        __syncthreads();
-        const uint32_t nl = nlist;
-        for (uint32_t k = 0; k < nl; ++k) {
-            const uint32_t seg = list[k];
+    const uint32_t M = counters[kCntM];
+    {
+        for (uint32_t k = blockIdx.x; k < M; k += gridDim.x) {
+            const uint32_t seg = mlist[k];
+            {
+                const uint32_t key0 = keys[seg_start[seg]];
+                if (key0 == sent || pack.d[table_of_key(pack, ntables, key0)].dim != D)
+                    continue;  // uniform across the workgroup
+            }
             const uint32_t p0 = partial_start[seg], np = partial_start[seg + 1] - p0;
             const uint32_t a = p0 + (uint32_t)((uint64_t)np * G / NG);
             const uint32_t b = p0 + (uint32_t)((uint64_t)np * (G + 1) / NG);
@@ -471,7 +469,7 @@ __global__ __launch_bounds__(256) void k_sgd_combine_generic(
 
 struct UpdateWs {
     uint32_t *ka, *va, *kb, *vb, *hist, *part, *flag, *seg_start, *nch, *multi, *chunk_seg,
-        *counters;
+        *counters, *mlist;
     float* partials;
     int64_t bytes;
 };
@@ -504,6 +502,7 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk)
     const int64_t max_chunks = n + n / chunk + 2;
     w.chunk_seg = (uint32_t*)take(4 * max_chunks);
     w.counters = (uint32_t*)take(4 * kCntSlots);
+    w.mlist = (uint32_t*)take(4 * (n / chunk + 2));
     const int64_t max_partials = 2 * (n / chunk) + 2;
     w.partials = (float*)take(4 * max_partials * (int64_t)(pdim > 0 ? pdim : 1));
     w.bytes = off;
@@ -520,6 +519,7 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
                              uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s) {
     const int64_t blocks = cdiv64(n, 256);
     const unsigned kb_grid = (unsigned)(blocks < 65536 ? blocks : 65536);
+    ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
     hipLaunchKernelGGL(k_build_keys, dim3(kb_grid), dim3(256), 0, s, pack, ntables, w.ka, w.va,
                        sent);
     ET_LAUNCH_CHECK("k_build_keys");
@@ -536,7 +536,7 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     ET_LAUNCH_CHECK("k_seg_start");
     const int64_t blocks1 = cdiv64(n + 1, 256);
     hipLaunchKernelGGL(k_seg_chunks, dim3((unsigned)blocks1), dim3(256), 0, s, w.seg_start, n,
-                       w.counters, chunk, w.nch, w.multi);
+                       w.counters, chunk, w.nch, w.multi, w.mlist);
     ET_LAUNCH_CHECK("k_seg_chunks");
     // nch -> chunk_start, multi -> partial_start (in place, n+1 entries)
     rc = exclusive_scan_u32(w.nch, w.nch, n + 1, w.part, s);
@@ -560,8 +560,8 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                            ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg,         \
                            w.multi, w.counters, chunk, w.partials, pdim, sent, eta32, eta64);  \
         hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,   \
-                           ntables, gr.keys, w.seg_start, w.multi, w.counters, w.partials,     \
-                           pdim, sent, eta32, eta64);                                          \
+                           ntables, gr.keys, w.seg_start, w.multi, w.counters, w.mlist,        \
+                           w.partials, pdim, sent, eta32, eta64);                              \
         break;
     switch (vec_dim) {
         ET_SGD_VEC(16)
