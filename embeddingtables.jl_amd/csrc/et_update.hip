@@ -49,26 +49,35 @@ __device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, ui
 }
 
 // 1. keys / values -----------------------------------------------------------
-__global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, int ntables,
+// Workgroup b works on table t with blk_off[t] <= b < blk_off[t+1] (host prefix of
+// workgroups per table), so the table is uniform and bags are read with 16-B loads
+// of consecutive occurrences.
+struct KeyGrid {
+    uint32_t blk_off[ET_MAX_TABLES_PER_LAUNCH + 1];
+};
+
+__global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg, int ntables,
                                                     uint32_t* __restrict__ keys,
                                                     uint32_t* __restrict__ vals, uint32_t sent) {
-    const uint32_t n = pack.occ_off[ntables];
-    for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < n;
-         o += (int64_t)gridDim.x * 256) {
-        int t = 0;
-        while (t + 1 < ntables && (uint32_t)o >= pack.occ_off[t + 1]) ++t;
-        const et_update_desc& d = pack.d[t];
-        const uint32_t ol = (uint32_t)o - pack.occ_off[t];
-        const uint32_t j = ol / (uint32_t)d.pool, i = ol - j * (uint32_t)d.pool;
+    int t = 0;
+    while (t + 1 < ntables && blockIdx.x >= kg.blk_off[t + 1]) ++t;
+    const et_update_desc& d = pack.d[t];
+    const uint32_t pool = (uint32_t)d.pool;
+    const uint32_t n_t = pool * (uint32_t)d.batch;
+    const uint32_t o0 = pack.occ_off[t], r0 = pack.row_off[t];
+    const uint64_t nr = (uint64_t)d.nrows;
+    const uint32_t nblk = kg.blk_off[t + 1] - kg.blk_off[t];
+    int bad = 0;
+    for (uint32_t ol = (blockIdx.x - kg.blk_off[t]) * 256u + threadIdx.x; ol < n_t;
+         ol += nblk * 256u) {
+        const uint32_t j = ol / pool, i = ol - j * pool;
         const uint64_t col = (uint64_t)(d.idx[(int64_t)j * d.ld_idx + i] - 1);
-        uint32_t key = sent;
-        if (col < (uint64_t)d.nrows)
-            key = pack.row_off[t] + (uint32_t)col;
-        else
-            note_oob();
-        keys[o] = key;
-        vals[o] = (uint32_t)o;
+        const bool ok = col < nr;
+        bad += ok ? 0 : 1;
+        keys[o0 + ol] = ok ? r0 + (uint32_t)col : sent;
+        vals[o0 + ol] = o0 + ol;
     }
+    if (bad) note_oob(bad);
 }
 
 // 3. segments ------------------------------------------------------------------
@@ -520,8 +529,18 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     const int64_t blocks = cdiv64(n, 256);
     const unsigned kb_grid = (unsigned)(blocks < 65536 ? blocks : 65536);
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
-    hipLaunchKernelGGL(k_build_keys, dim3(kb_grid), dim3(256), 0, s, pack, ntables, w.ka, w.va,
-                       sent);
+    KeyGrid kg;
+    kg.blk_off[0] = 0;
+    for (int t = 0; t < ntables; ++t) {
+        const int64_t nt = pack.occ_off[t + 1] - pack.occ_off[t];
+        int64_t nb = cdiv64(nt, 256);
+        nb = nb < 2048 ? nb : 2048;  // grid-stride beyond 2048 workgroups per table
+        kg.blk_off[t + 1] = kg.blk_off[t] + (uint32_t)nb;
+    }
+    (void)kb_grid;
+    if (kg.blk_off[ntables] > 0)
+        hipLaunchKernelGGL(k_build_keys, dim3(kg.blk_off[ntables]), dim3(256), 0, s, pack, kg,
+                           ntables, w.ka, w.va, sent);
     ET_LAUNCH_CHECK("k_build_keys");
     SortBuffers sb{w.ka, w.va, w.kb, w.vb, w.hist, w.part};
     int rc = radix_sort_pairs(sb, n, bits_for(sent), &out.keys, &out.vals, s);
@@ -553,7 +572,10 @@ template <int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, float eta32, double eta64,
                      int vec_dim, bool any_generic, hipStream_t s) {
-    const unsigned grid = 256 * 8;
+    static const unsigned grid = [] {
+        const char* e = getenv("ET_SGD_GRID");  // experiments: workgroups of the SGD passes
+        return e ? (unsigned)atoi(e) : 256u * 16u;
+    }();
 #define ET_SGD_VEC(DD)                                                                         \
     case DD:                                                                                   \
         hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
