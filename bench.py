@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--no-check", action="store_true", help="skip the CPU/GPU bit comparison")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the config-2 (gather) and config-4 (Zipf + SGD) measurements")
+    p.add_argument("--force-shard", action="store_true",
+                   help="use the sharded (all-gather + concat) step even on one rank")
     p.add_argument("--subset", choices=["all", "heavy", "light"], default="all",
                    help="calibration only: tables above / below 4 MiB")
     p.add_argument("--rows", type=int, default=0,
@@ -281,7 +283,7 @@ def main():
     dst = torch.empty((B, layout.ld), dtype=torch.float32, device=device)
     strat = et.PreallocationStrategy(0)
     sharded = ShardedPreallocation(layout, rank, world, B, torch.float32, device) \
-        if world > 1 else None
+        if world > 1 or args.force_shard else None
 
     def step():
         if sharded is None:
@@ -371,7 +373,7 @@ def main():
             "kernel_ms": kernel_ms,
         },
     }
-    if world > 1:
+    if sharded is not None:
         result["lookup_only_ms"] = kernel_ms
     if world == 1 and not args.no_extra:
         result["config2_gather"] = bench_config2(et, L, device, 50, 5)
