@@ -343,8 +343,19 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
     }
 }
 
-// Generic path: any feature size / alignment / per-table dims.  One wave per bag,
-// lanes stride over the features, pool order sequential per feature.
+// Address of column `row` (0-based) of a contiguous or paged (SplitEmbedding) table.
+template <typename T>
+__device__ __forceinline__ T* col_ptr(const void* table, int64_t ld, int64_t cols_per_page,
+                                      uint64_t row) {
+    if (cols_per_page > 0) {
+        T* const* pages = reinterpret_cast<T* const*>(table);
+        return pages[row / (uint64_t)cols_per_page] + (row % (uint64_t)cols_per_page) * ld;
+    }
+    return (T*)table + row * (uint64_t)ld;
+}
+
+// Generic path: any feature size / alignment / per-table dims / paged tables.  One wave
+// per bag, lanes stride over the features, pool order sequential per feature.
 template <typename T, typename A, bool NT>
 __global__ __launch_bounds__(256) void k_pooled_generic(LookupPack pack, int ntables,
                                                         int64_t batch, T* __restrict__ dst,
@@ -370,7 +381,7 @@ __global__ __launch_bounds__(256) void k_pooled_generic(LookupPack pack, int nta
             const bool ok = row < (uint64_t)d.nrows;
             if (!ok && lane == 0 && f0 == 0) note_oob();
             row = ok ? row : 0;
-            const T* src = table + row * (uint64_t)d.ld_table;
+            const T* src = col_ptr<const T>(d.table, d.ld_table, d.cols_per_page, row);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int f = f0 + lane + 64 * k;
@@ -646,8 +657,8 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
     if (!dst) return fail(ET_ERR_ARG, "dst is NULL");
     for (int t = 0; t < ntables; ++t) {
         const et_lookup_desc& d = descs[t];
-        if (d.dim < 0 || d.pool < 0 || d.nrows < 0)
-            return fail(ET_ERR_ARG, "table %d: negative dim/pool/nrows", t);
+        if (d.dim < 0 || d.pool < 0 || d.nrows < 0 || d.cols_per_page < 0)
+            return fail(ET_ERR_ARG, "table %d: negative dim/pool/nrows/cols_per_page", t);
         if (d.dim == 0) continue;
         if (d.ld_table < d.dim) return fail(ET_ERR_ARG, "table %d: ld_table < dim", t);
         if (d.dst_row_off < 0 || d.dst_row_off + d.dim > ld_dst)
@@ -674,6 +685,8 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
                         ((ld_dst * es) % 16 == 0);
         if (d.dim == 0) {
             kind_of[t] = -1;
+        } else if (d.cols_per_page != 0) {
+            kind_of[t] = kGeneric;  // paged (SplitEmbedding) tables: layout-agnostic kernel
         } else if (d.pool == 1 && al && gather_rb_ok((int64_t)d.dim * es)) {
             kind_of[t] = kGather;
         } else if (d.pool >= 1 && al && vec_dim_ok(d.dim) && d.nrows < 0xffffffffll &&
@@ -735,6 +748,7 @@ extern "C" int et_gather(int dtype, const void* table, int64_t ld_table, int64_t
     d.idx = idx;
     d.ld_idx = 1;
     d.dst_row_off = 0;
+    d.cols_per_page = 0;
     // A non-reducing lookup is a bit copy whatever the dtype: never the fp32-acc mode.
     return et::lookup_dispatch(dtype, &d, 1, n, dst, ld_dst, flags & ~ET_FLAG_F16_FP32_ACC,
                                static_cast<hipStream_t>(stream));
@@ -756,6 +770,7 @@ extern "C" int et_pooled_sum(int dtype, const void* table, int64_t ld_table, int
     d.idx = idx;
     d.ld_idx = ld_idx;
     d.dst_row_off = 0;
+    d.cols_per_page = 0;
     // pool == 1 as a *matrix* index is still a sum of one row == that row.
     return et::lookup_dispatch(dtype, &d, 1, batch, dst, ld_dst,
                                pool == 1 ? (flags & ~ET_FLAG_F16_FP32_ACC) : flags,

@@ -34,6 +34,7 @@ constexpr uint32_t kChunk = 512;  // occurrences per chunk (non-exact mode)
 
 struct UpdatePack {
     et_update_desc d[ET_MAX_TABLES_PER_LAUNCH];
+    uint32_t vec_mask;  // bit t: table t is updated by the vector kernels (else generic)
     uint32_t row_off[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of nrows
     uint32_t occ_off[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of pool * batch
 };
@@ -283,7 +284,7 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
             if (qq + g >= nq || kkey == sent) continue;  // past the end / bad indices
             const int t = table_of_key(pack, ntables, kkey);
             const et_update_desc& d = pack.d[t];
-            if (d.dim != D) continue;  // another dim group's launch
+            if (!((pack.vec_mask >> t) & 1u)) continue;  // the generic kernels' table
             float* w = reinterpret_cast<float*>(d.table) +
                        (uint64_t)(kkey - pack.row_off[t]) * (uint64_t)d.ld_table;
             u32x4 x[NV];
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
             const uint32_t seg = mlist[k];
             {
                 const uint32_t key0 = keys[seg_start[seg]];
-                if (key0 == sent || pack.d[table_of_key(pack, ntables, key0)].dim != D)
+                if (key0 == sent || !((pack.vec_mask >> table_of_key(pack, ntables, key0)) & 1u))
                     continue;  // uniform across the workgroup
             }
             const uint32_t p0 = partial_start[seg], np = partial_start[seg + 1] - p0;
@@ -411,7 +412,7 @@ __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
     const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_seg,
     const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ counters,
     uint32_t chunk, float* __restrict__ partials, int pdim, uint32_t sent, float eta32,
-    double eta64, int skip_dim) {
+    double eta64) {
     const int lane = threadIdx.x & 63;
     const uint32_t C = counters[kCntC];
     const uint32_t waves = gridDim.x * 4;
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
         if (key == sent) continue;
         const int t = table_of_key(pack, ntables, key);
         const et_update_desc& d = pack.d[t];
-        if (d.dim == skip_dim) continue;  // handled by the vector kernel
+        if ((pack.vec_mask >> t) & 1u) continue;  // handled by the vector kernel
         const uint32_t s0 = seg0 + pidx * chunk;
         const uint32_t s1 = s0 + chunk < seg1 ? s0 + chunk : seg1;
         const float* delta = reinterpret_cast<const float*>(d.delta);
@@ -435,8 +436,8 @@ __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
                 acc = acc + delta[(uint64_t)bag * (uint64_t)d.ld_delta + f];
             }
             if (nchunks == 1) {
-                float* w = reinterpret_cast<float*>(d.table) +
-                           (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table + f;
+                float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
+                                          key - pack.row_off[t]) + f;
                 store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
             } else {
                 partials[(uint64_t)(partial_start[u] + pidx) * pdim + f] = acc;
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256) void k_sgd_combine_generic(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
     const uint32_t* __restrict__ counters, const float* __restrict__ partials, int pdim,
-    uint32_t sent, float eta32, double eta64, int skip_dim) {
+    uint32_t sent, float eta32, double eta64) {
     const int lane = threadIdx.x & 63;
     const uint32_t Useg = counters[kCntU];
     const uint32_t waves = gridDim.x * 4;
@@ -461,12 +462,12 @@ __global__ __launch_bounds__(256) void k_sgd_combine_generic(
         if (key == sent) continue;
         const int t = table_of_key(pack, ntables, key);
         const et_update_desc& d = pack.d[t];
-        if (d.dim == skip_dim) continue;
+        if ((pack.vec_mask >> t) & 1u) continue;
         for (int f = lane; f < d.dim; f += 64) {
             float acc = 0.0f;
             for (uint32_t q = p0; q < p1; ++q) acc = acc + partials[(uint64_t)q * pdim + f];
-            float* w = reinterpret_cast<float*>(d.table) +
-                       (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table + f;
+            float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
+                                      key - pack.row_off[t]) + f;
             store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
         }
     }
@@ -599,10 +600,10 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     if (any_generic) {
         hipLaunchKernelGGL((k_sgd_chunks_generic<MODE, NT>), dim3(grid), dim3(256), 0, s, pack,
                            ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg, w.multi,
-                           w.counters, chunk, w.partials, pdim, sent, eta32, eta64, vec_dim);
+                           w.counters, chunk, w.partials, pdim, sent, eta32, eta64);
         hipLaunchKernelGGL((k_sgd_combine_generic<MODE, NT>), dim3(grid), dim3(256), 0, s, pack,
                            ntables, gr.keys, w.seg_start, w.multi, w.counters, w.partials, pdim,
-                           sent, eta32, eta64, vec_dim);
+                           sent, eta32, eta64);
         ET_LAUNCH_CHECK("k_sgd_chunks_generic");
     }
     return ET_OK;
@@ -619,7 +620,7 @@ inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_
     int pdim = 0;
     for (int t = 0; t < ntables; ++t) {
         const et_update_desc& d = descs[t];
-        if (d.dim < 0 || d.pool < 0 || d.nrows < 0 || d.batch < 0)
+        if (d.dim < 0 || d.pool < 0 || d.nrows < 0 || d.batch < 0 || d.cols_per_page < 0)
             return fail(ET_ERR_ARG, "table %d: negative size", t);
         if (d.pool > 0 && d.batch > 0) {
             if (!d.table || !d.delta || !d.idx) return fail(ET_ERR_ARG, "table %d: NULL", t);
@@ -681,6 +682,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     uint32_t ro = 0, oo = 0;
     int vec_dim = -1;
     bool any_generic = false;
+    pack.vec_mask = 0;
     for (int t = 0; t < ntables; ++t) {
         const et_update_desc& d = descs[t];
         pack.d[t] = d;
@@ -689,29 +691,20 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         ro += (uint32_t)d.nrows;
         oo += (uint32_t)(d.pool * d.batch);
         if (d.pool == 0 || d.batch == 0 || d.dim == 0) continue;
-        const bool al = et::aligned16(d.table) && et::aligned16(d.delta) &&
-                        (d.ld_table % 4 == 0) && (d.ld_delta % 4 == 0) && et::vec_dim_ok(d.dim);
-        if (al && (vec_dim < 0 || vec_dim == d.dim))
+        const bool vec_ok = d.cols_per_page == 0 && et::aligned16(d.table) &&
+                            et::aligned16(d.delta) && (d.ld_table % 4 == 0) &&
+                            (d.ld_delta % 4 == 0) && et::vec_dim_ok(d.dim) &&
+                            (vec_dim < 0 || vec_dim == d.dim);
+        if (vec_ok) {
             vec_dim = d.dim;
-        else
+            pack.vec_mask |= 1u << t;
+        } else {
             any_generic = true;
+        }
     }
     pack.row_off[ntables] = ro;
     pack.occ_off[ntables] = oo;
     const uint32_t sent = ro;  // key of out-of-range occurrences (sorts last)
-    if (vec_dim < 0) any_generic = true;
-    // A table of vec_dim that is misaligned must not be taken by the vector kernel: the
-    // generic kernels skip only `vec_dim`, so route such tables by disabling vec.
-    for (int t = 0; t < ntables && vec_dim > 0; ++t) {
-        const et_update_desc& d = descs[t];
-        if (d.dim != vec_dim || d.pool == 0 || d.batch == 0) continue;
-        const bool al = et::aligned16(d.table) && et::aligned16(d.delta) &&
-                        (d.ld_table % 4 == 0) && (d.ld_delta % 4 == 0);
-        if (!al) {
-            vec_dim = -1;
-            any_generic = true;
-        }
-    }
 
     et::Grouped gr;
     rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s);
@@ -875,6 +868,7 @@ extern "C" int et_index_build(const int64_t* idx, int32_t pool, int64_t ld_idx, 
     d.ld_idx = ld_idx;
     d.batch = batch;
     pack.d[0] = d;
+    pack.vec_mask = 0;
     pack.row_off[0] = 0;
     pack.row_off[1] = (uint32_t)nrows;
     pack.occ_off[0] = 0;
@@ -914,7 +908,7 @@ namespace et {
 
 template <int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_update_indexed(
-    float* __restrict__ table, int64_t ld_table, int64_t nrows, int dim,
+    void* __restrict__ table, int64_t ld_table, int64_t cols_per_page, int64_t nrows, int dim,
     const float* __restrict__ delta, int64_t ld_delta, const int64_t* __restrict__ cum_col,
     const int64_t* __restrict__ cum_off, int64_t ubegin, int64_t uend,
     const int64_t* __restrict__ map, float eta32, double eta64) {
@@ -927,7 +921,7 @@ __global__ __launch_bounds__(256) void k_update_indexed(
             continue;
         }
         const int64_t k0 = cum_off[e] - 1, k1 = cum_off[e + 1] - 1;
-        float* w = table + col * (uint64_t)ld_table;
+        float* w = col_ptr<float>(table, ld_table, cols_per_page, col);
         for (int f = lane; f < dim; f += 64) {
             float acc = 0.0f;  // zero(Tiled) / zero!(scratchspace)
             for (int64_t k = k0; k < k1; ++k)
@@ -939,15 +933,15 @@ __global__ __launch_bounds__(256) void k_update_indexed(
 
 }  // namespace et
 
-extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table, int64_t nrows,
-                                 int32_t dim, const void* delta, int64_t ld_delta,
+extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
+                                 int64_t cols_per_page, int64_t nrows, int32_t dim, const void* delta, int64_t ld_delta,
                                  const int64_t* cumulative_col, const int64_t* cumulative_off,
                                  int64_t ubegin, int64_t uend, const int64_t* map, double eta,
                                  uint32_t flags, void* stream) {
     et::clear_err();
     if (dtype != ET_F32) return et::fail(ET_ERR_UNSUPPORTED, "update supports ET_F32 only");
     if (uend <= ubegin || dim == 0) return ET_OK;
-    if (ubegin < 0 || dim < 0 || ld_table < dim || ld_delta < dim)
+    if (ubegin < 0 || dim < 0 || ld_table < dim || ld_delta < dim || cols_per_page < 0)
         return et::fail(ET_ERR_ARG, "bad sizes");
     if (!table || !delta || !cumulative_col || !cumulative_off || !map)
         return et::fail(ET_ERR_ARG, "NULL argument");
@@ -958,9 +952,9 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table, int64
     const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;
     const float eta32 = (float)eta;
 #define ET_UI(M, NTV)                                                                             \
-    hipLaunchKernelGGL((et::k_update_indexed<M, NTV>), dim3(grid), dim3(256), 0, s, (float*)table, \
-                       ld_table, nrows, dim, (const float*)delta, ld_delta, cumulative_col,       \
-                       cumulative_off, ubegin, uend, map, eta32, eta)
+    hipLaunchKernelGGL((et::k_update_indexed<M, NTV>), dim3(grid), dim3(256), 0, s, table,      \
+                       ld_table, cols_per_page, nrows, dim, (const float*)delta, ld_delta,       \
+                       cumulative_col, cumulative_off, ubegin, uend, map, eta32, eta)
     if (mode == 0) {
         if (nt) ET_UI(0, true); else ET_UI(0, false);
     } else if (mode == 1) {

@@ -9,8 +9,8 @@ and fails if it has not been built.
 from . import _lib
 from ._lib import EmbtabError, check_errors
 from .tables import (AbstractEmbeddingTable, AbstractLookupType, ArgumentError, Dynamic,
-                     Forward, IndexingContext, NoContext, SimpleEmbedding, Static, Update,
-                     columnpointer, example, featuresize)
+                     Forward, IndexingContext, NoContext, SimpleEmbedding, SplitEmbedding, Static,
+                     Update, columnpointer, example, featuresize)
 from .lookup import (AbstractExecutionStrategy, DefaultStrategy, NoTangent,
                      PreallocationStrategy, SimpleParallelStrategy, colwrap, destination, lookup,
                      lookup_, maplookup, maplookup_)
@@ -22,8 +22,8 @@ _lib.load()
 
 __all__ = [
     "AbstractEmbeddingTable", "AbstractLookupType", "ArgumentError", "Dynamic", "Static",
-    "IndexingContext", "NoContext", "Forward", "Update", "SimpleEmbedding", "featuresize",
-    "example", "columnpointer", "AbstractExecutionStrategy", "DefaultStrategy",
+    "IndexingContext", "NoContext", "Forward", "Update", "SimpleEmbedding", "SplitEmbedding",
+    "featuresize", "example", "columnpointer", "AbstractExecutionStrategy", "DefaultStrategy",
     "SimpleParallelStrategy", "PreallocationStrategy", "NoTangent", "colwrap", "destination",
     "lookup", "lookup_", "maplookup", "maplookup_", "SparseEmbeddingUpdate", "uncompress",
     "rrule", "Descent", "AbstractIndexer", "Indexer", "SparseIndexer", "DenseIndexer",

@@ -21,7 +21,7 @@ ET_FLAG_EXACT_UPDATE = 4
 ET_FLAG_SGD_UNFUSED = 8
 ET_FLAG_SGD_F64_ALPHA = 16
 ET_MAX_TABLES_PER_LAUNCH = 32
-ET_ABI_VERSION = 1
+ET_ABI_VERSION = 2
 
 TORCH_TO_ET = {
     torch.float32: ET_F32,
@@ -66,6 +66,7 @@ class LookupDesc(ctypes.Structure):
         ("idx", ctypes.c_void_p),
         ("ld_idx", ctypes.c_int64),
         ("dst_row_off", ctypes.c_int64),
+        ("cols_per_page", ctypes.c_int64),
     ]
 
 
@@ -83,6 +84,7 @@ class UpdateDesc(ctypes.Structure):
         ("idx", ctypes.c_void_p),
         ("ld_idx", ctypes.c_int64),
         ("batch", ctypes.c_int64),
+        ("cols_per_page", ctypes.c_int64),
     ]
 
 
@@ -112,7 +114,7 @@ def load() -> ctypes.CDLL:
         "et_sparse_sgd": ([c_int, vp, i32, dbl, u32, vp, i64, vp], c_int),
         "et_index_workspace_size": ([i64, vp], c_int),
         "et_index_build": ([vp, i32, i64, i64, i64, vp, vp, vp, vp, vp, i64, vp], c_int),
-        "et_update_indexed": ([c_int, vp, i64, i64, i32, vp, i64, vp, vp, i64, i64, vp, dbl, u32,
+        "et_update_indexed": ([c_int, vp, i64, i64, i64, i32, vp, i64, vp, vp, i64, i64, vp, dbl, u32,
                                vp], c_int),
         "et_concat_slabs": ([c_int, vp, i32, i64, i64, vp, vp, vp, i64, vp], c_int),
         "et_fill_uniform": ([c_int, vp, i64, u64, u64, dbl, dbl, vp], c_int),

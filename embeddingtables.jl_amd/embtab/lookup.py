@@ -135,7 +135,16 @@ def lookup_(dst: torch.Tensor, A: AbstractEmbeddingTable, I: torch.Tensor,
     L = _lib.load()
     D, R = A.size()
     flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
-    if I.dim() == 1:
+    table, cpp = A.device_table()
+    if cpp:
+        # paged table (SplitEmbedding): the descriptor entry point addresses pages
+        descs = (_lib.LookupDesc * 1)()
+        descs[0] = _lib.LookupDesc(table, A.ld, R, D, 1 if I.dim() == 1 else int(I.shape[1]),
+                                   I.data_ptr(), 1 if I.dim() == 1 else _ld(I), 0, cpp)
+        rc = L.et_maplookup_prealloc(_lib.et_dtype(dst), ctypes.addressof(descs), 1, B,
+                                     dst.data_ptr(), _ld(dst), flags,
+                                     _lib.stream_handle(dst.device))
+    elif I.dim() == 1:
         rc = L.et_gather(_lib.et_dtype(dst), A.columnpointer(1), A.ld, R, D, I.data_ptr(), B,
                          dst.data_ptr(), _ld(dst), flags, _lib.stream_handle(dst.device))
     else:
@@ -226,8 +235,9 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
             raise ArgumentError(f"table {t}: batch {_trailing_size(i)} != {B}")
         D, R = A.size()
         pool = 1 if i.dim() == 1 else int(i.shape[1])
-        descs[t] = _lib.LookupDesc(A.columnpointer(1), A.ld, R, D, pool, i.data_ptr(),
-                                   1 if i.dim() == 1 else _ld(i), off)
+        table, cpp = A.device_table()
+        descs[t] = _lib.LookupDesc(table, A.ld, R, D, pool, i.data_ptr(),
+                                   1 if i.dim() == 1 else _ld(i), off, cpp)
         off += D
     flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
     _lib.check(_lib.load().et_maplookup_prealloc(

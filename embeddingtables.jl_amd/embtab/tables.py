@@ -99,6 +99,11 @@ class AbstractEmbeddingTable:
     def example(self) -> torch.Tensor:
         raise NotImplementedError
 
+    def device_table(self) -> tuple[int, int]:
+        """``(table, cols_per_page)`` for an et_lookup_desc / et_update_desc: the first
+        column's address and 0 for a contiguous table (the default)."""
+        return self.columnpointer(1), 0
+
     @property
     def dtype(self):
         return self.example().dtype
@@ -180,6 +185,114 @@ class SimpleEmbedding(AbstractEmbeddingTable):
 
     def parent(self) -> torch.Tensor:
         return self.data
+
+
+class SplitEmbedding(AbstractEmbeddingTable):
+    """A table whose columns are stored in separately allocated pages of
+    ``cols_per_shard`` columns each (src/split.jl:3-86).
+
+    ``SplitEmbedding(data, cols_per_shard)`` copies a ``(R, D)`` tensor into
+    ``ceil(R / cols_per_shard)`` page tensors (the last one may be short), like the
+    reference's inner constructor (src/split.jl:11-26); the lookup type is always
+    ``Static(D)``.  The kernels address a column through a device array of page
+    pointers (``et_lookup_desc.cols_per_page``), so a paged table is looked up and
+    updated by the same launches as a contiguous one."""
+
+    def __init__(self, data: torch.Tensor, cols_per_shard: int = 1):
+        if not isinstance(data, torch.Tensor) or data.dim() != 2:
+            raise ArgumentError("SplitEmbedding expects a 2-D (ncols, featuresize) tensor")
+        if int(cols_per_shard) < 1:
+            raise ArgumentError("cols_per_shard must be positive")
+        cps = int(cols_per_shard)
+        R = int(data.shape[0])
+        pages = [data[s:min(s + cps, R)].clone(memory_format=torch.contiguous_format)
+                 for s in range(0, R, cps)]
+        self._init(pages, int(data.shape[1]), cps, data.dtype, data.device)
+
+    @classmethod
+    def undef(cls, featuresize: int, ncols: int, cols_per_shard: int = 1,
+              dtype=torch.float32, device="cuda", lookup_type: AbstractLookupType | None = None):
+        """``SplitEmbedding{S,T}(undef, featuresize, ncols, cols_per_shard)``
+        (src/split.jl:29-46); ``lookup_type = Static(N)`` must match ``featuresize``."""
+        if isinstance(lookup_type, Static) and lookup_type.N != featuresize:
+            raise ArgumentError(f"Static{{{lookup_type.N}}} != featuresize {featuresize}")
+        cps = int(cols_per_shard)
+        if cps < 1:
+            raise ArgumentError("cols_per_shard must be positive")
+        self = cls.__new__(cls)
+        pages = [torch.empty((min(cps, ncols - s), featuresize), dtype=dtype, device=device)
+                 for s in range(0, ncols, cps)]
+        self._init(pages, featuresize, cps, dtype, device)
+        if lookup_type is not None:
+            self.lookup_type = lookup_type
+        return self
+
+    def _init(self, pages, D, cps, dtype, device):
+        if not pages:
+            raise ArgumentError("a SplitEmbedding needs at least one column")
+        self.pages = pages
+        self.matrixsize = (D, cps)
+        self.lookup_type = Static(D)
+        # the device page table the kernels read: one 8-byte pointer per page
+        self.page_table = torch.tensor([p.data_ptr() for p in pages], dtype=torch.int64,
+                                       device=device)
+
+    def __repr__(self):
+        d, r = self.size()
+        return (f"{d}x{r} SplitEmbedding{{{self.lookup_type!r}, {self.dtype}}} "
+                f"({len(self.pages)} pages of {self.matrixsize[1]})")
+
+    def size(self):
+        D, cps = self.matrixsize
+        return (D, cps * (len(self.pages) - 1) + int(self.pages[-1].shape[0]))
+
+    @property
+    def ld(self) -> int:
+        return self.matrixsize[0]
+
+    @property
+    def cols_per_page(self) -> int:
+        return self.matrixsize[1]
+
+    def _page_col(self, i: int):
+        """``_divrem_index(i, shardsize)`` (src/split.jl:54-60), 0-based page/column."""
+        return divmod(i - 1, self.matrixsize[1])
+
+    def columnpointer(self, i: int, ctx: IndexingContext | None = None) -> int:
+        """src/split.jl:81-86."""
+        p, c = self._page_col(i)
+        if not 0 <= p < len(self.pages):
+            raise IndexError(f"BoundsError: column {i} outside {self.size()}")
+        page = self.pages[p]
+        return page.data_ptr() + c * self.ld * page.element_size()
+
+    def device_table(self) -> tuple[int, int]:
+        return self.page_table.data_ptr(), self.matrixsize[1]
+
+    def example(self) -> torch.Tensor:
+        return self.pages[0]
+
+    def _col(self, j: int) -> torch.Tensor:
+        p, c = self._page_col(j)
+        return self.pages[p][c]
+
+    def copy_(self, src: torch.Tensor) -> "SplitEmbedding":
+        """``table .= base`` for a ``(R, D)`` tensor."""
+        cps = self.matrixsize[1]
+        for k, page in enumerate(self.pages):
+            page.copy_(src[k * cps:k * cps + page.shape[0]])
+        return self
+
+    def to_dense(self) -> torch.Tensor:
+        """All columns as one ``(R, D)`` tensor (``collect``)."""
+        return torch.cat(self.pages, 0)
+
+    def zeros(self) -> "SplitEmbedding":
+        z = SplitEmbedding.undef(self.matrixsize[0], self.size()[1], self.matrixsize[1],
+                                 self.dtype, self.device)
+        for p in z.pages:
+            p.zero_()
+        return z
 
 
 def featuresize(x) -> int:

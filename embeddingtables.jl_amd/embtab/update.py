@@ -229,8 +229,9 @@ def _update_desc(table: AbstractEmbeddingTable, grad: SparseEmbeddingUpdate) -> 
         raise ArgumentError(f"gradient shape {tuple(delta.shape)} != ({B}, {D})")
     if delta.numel() > 0 and delta.stride(1) != 1:
         raise ArgumentError("gradient features must be contiguous")
-    return _lib.UpdateDesc(table.columnpointer(1), table.ld, R, D, P, delta.data_ptr(), _ld(delta),
-                           I.data_ptr(), 1 if I.dim() == 1 else _ld(I), B)
+    tp, cpp = table.device_table()
+    return _lib.UpdateDesc(tp, table.ld, R, D, P, delta.data_ptr(), _ld(delta),
+                           I.data_ptr(), 1 if I.dim() == 1 else _ld(I), B, cpp)
 
 
 def _sparse_sgd(descs, eta: float, flags: int, device):
@@ -324,8 +325,9 @@ def _update_from_indexer(table, grad: SparseEmbeddingUpdate, indexer: AbstractIn
     D, R = table.size()
     cum = base.cumulative  # (U+1, 2) view of the (2, n+1) buffer
     fused = fused_update_path(table)
+    tp, cpp = table.device_table()
     _lib.check(_lib.load().et_update_indexed(
-        _lib.ET_F32, table.columnpointer(1), table.ld, R, D, delta.data_ptr(), _ld(delta),
+        _lib.ET_F32, tp, table.ld, cpp, R, D, delta.data_ptr(), _ld(delta),
         cum[:, 0].data_ptr(), cum[:, 1].data_ptr(), b, e, base.map.data_ptr(), alpha,
         _sgd_flags(fused, nontemporal), _lib.stream_handle(table.device)))
 

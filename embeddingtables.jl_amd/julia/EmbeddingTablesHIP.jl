@@ -90,6 +90,13 @@ function Base.setindex!(A::HipArray{T}, v, i::Int) where {T}
     return v
 end
 Base.IndexStyle(::Type{<:HipArray}) = IndexLinear()
+# Host array -> new device array (hipMemcpyHostToDevice).
+function upload(A::Array{T,N}) where {T,N}
+    D = HipArray{T,N}(undef, size(A))
+    ccall((:hipMemcpy, libhip), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Cint),
+          D.ptr, A, sizeof(A), 1) == 0 || error("hipMemcpy failed")
+    return D
+end
 
 #####
 ##### The table type (AbstractEmbeddingTable contract, README.md:288-307)
@@ -112,6 +119,34 @@ Base.setindex!(A::HipEmbedding, v, i::Int) = (A.data[i] = v)
 columnpointer(A::HipEmbedding{S,T}, i::Integer) where {S,T} =
     A.data.ptr + (i - 1) * leading(A.data) * sizeof(T)
 example(A::HipEmbedding) = A.data
+
+# Paged table: the reference's SplitEmbedding (src/split.jl:3-86) with its pages on the
+# device.  `pagetable` holds the pages' device addresses; the kernels address column r
+# as pages[(r-1) ÷ cps] + ((r-1) % cps) * featuresize (et_lookup_desc.cols_per_page).
+struct HipSplitEmbedding{S,T} <: AbstractEmbeddingTable{S,T}
+    pages::Vector{HipMatrix{T}}
+    pagetable::HipVector{UInt64}
+    matrixsize::Tuple{Int,Int}
+end
+function HipSplitEmbedding(A::Matrix{T}, cols_per_shard = 1) where {T}
+    n = size(A, 2)
+    pages = [upload(A[:, s:min(s + cols_per_shard - 1, n)]) for s in 1:cols_per_shard:n]
+    pt = upload(UInt64[UInt64(p.ptr) for p in pages])
+    return HipSplitEmbedding{Static{size(A, 1)},T}(pages, pt, (size(A, 1), cols_per_shard))
+end
+Base.size(A::HipSplitEmbedding) =
+    (A.matrixsize[1], A.matrixsize[2] * (length(A.pages) - 1) + size(last(A.pages), 2))
+function columnpointer(A::HipSplitEmbedding{S,T}, i::Integer) where {S,T}
+    page, col = divrem(i - 1, A.matrixsize[2])
+    return A.pages[page + 1].ptr + col * A.matrixsize[1] * sizeof(T)
+end
+example(A::HipSplitEmbedding) = first(A.pages)
+
+# (table, ld, cols_per_page) of an et_*_desc: contiguous tables pass cols_per_page = 0.
+_device_table(A::HipEmbedding) = (Ptr{Cvoid}(A.data.ptr), leading(A.data), 0)
+_device_table(A::HipSplitEmbedding) = (Ptr{Cvoid}(A.pagetable.ptr), A.matrixsize[1],
+                                       A.matrixsize[2])
+const HipTable{S,T} = Union{HipEmbedding{S,T},HipSplitEmbedding{S,T}}
 
 # Preallocation gradients are row blocks of one big matrix: a view's leading dimension.
 _ptr_ld(A::HipMatrix) = (Ptr{Cvoid}(A.ptr), leading(A))
@@ -158,17 +193,30 @@ struct LookupDesc
     idx::Ptr{Int64}
     ld_idx::Int64
     dst_row_off::Int64
+    cols_per_page::Int64
+end
+
+# A paged table's single-table lookup! goes through the descriptor entry point.
+function lookup!(dst, A::HipSplitEmbedding{S,T}, I::Union{HipVector{Int},HipMatrix{Int}}) where {S,T}
+    p, ld = _ptr_ld(dst)
+    tp, ldt, cpp = _device_table(A)
+    pool = ndims(I) == 1 ? 1 : size(I, 1)
+    desc = [LookupDesc(tp, ldt, size(A, 2), size(A, 1), pool, I.ptr, pool, 0, cpp)]
+    check(ccall((:et_maplookup_prealloc, libembtab), Cint,
+                (Cint, Ptr{LookupDesc}, Int32, Int64, Ptr{Cvoid}, Int64, UInt32, Ptr{Cvoid}),
+                et_dtype(T), desc, 1, size(I, ndims(I)), p, ld, ET_FLAG_NONTEMPORAL, stream()))
+    return dst
 end
 
 function maplookup!(strategy::PreallocationStrategy, dst::HipMatrix{T},
-                    x::Vector{<:HipEmbedding{<:Any,T}}, I0; kw...) where {T}
+                    x::Vector{<:HipTable{<:Any,T}}, I0; kw...) where {T}
     I = EmbeddingTables.colwrap(I0)
     descs = Vector{LookupDesc}(undef, length(x))
     off = strategy.prependrows
     for (t, (A, i)) in enumerate(zip(x, I))
         pool = ndims(i) == 1 ? 1 : size(i, 1)
-        descs[t] = LookupDesc(A.data.ptr, leading(A.data), size(A, 2), size(A, 1), pool,
-                              pointer(i), pool, off)
+        tp, ldt, cpp = _device_table(A)
+        descs[t] = LookupDesc(tp, ldt, size(A, 2), size(A, 1), pool, pointer(i), pool, off, cpp)
         off += size(A, 1)
     end
     check(ccall((:et_maplookup_prealloc, libembtab), Cint,
@@ -193,20 +241,22 @@ struct UpdateDesc
     idx::Ptr{Int64}
     ld_idx::Int64
     batch::Int64
+    cols_per_page::Int64
 end
 
-function _update_desc(A::HipEmbedding{S,Float32}, g::SparseEmbeddingUpdate) where {S}
+function _update_desc(A::HipTable{S,Float32}, g::SparseEmbeddingUpdate) where {S}
     dp, dld = _ptr_ld(g.delta)
     I = g.indices
     pool = ndims(I) == 1 ? 1 : size(I, 1)
-    return UpdateDesc(A.data.ptr, leading(A.data), size(A, 2), size(A, 1), pool, dp, dld,
-                      pointer(I), pool, size(I, ndims(I)))
+    tp, ldt, cpp = _device_table(A)
+    return UpdateDesc(tp, ldt, size(A, 2), size(A, 1), pool, dp, dld, pointer(I), pool,
+                      size(I, ndims(I)), cpp)
 end
 
 # The reference picks its fused `muladd` kernel for Static tables of <= 512 bytes per
 # column (src/sparseupdate.jl:131-154), the generic `x - alpha*y` path otherwise.
-_fused(::HipEmbedding{Static{N},T}) where {N,T} = N * sizeof(T) <= 512
-_fused(::HipEmbedding) = false
+_fused(::HipTable{Static{N},T}) where {N,T} = N * sizeof(T) <= 512
+_fused(::HipTable) = false
 
 const WORKSPACE = Ref{Any}(nothing)
 function _workspace(nbytes)
@@ -228,7 +278,7 @@ function _sparse_sgd(descs::Vector{UpdateDesc}, eta::Float64, flags::UInt32)
                 ET_F32, descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
 end
 
-function update!(opt::Flux.Descent, table::HipEmbedding{S,Float32}, grad::SparseEmbeddingUpdate,
+function update!(opt::Flux.Descent, table::HipTable{S,Float32}, grad::SparseEmbeddingUpdate,
                  indexer = Indexer(), ::Val{Nontemporal} = Val(true), args...) where {S,Nontemporal}
     flags = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
             (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED)
@@ -237,7 +287,7 @@ function update!(opt::Flux.Descent, table::HipEmbedding{S,Float32}, grad::Sparse
     return nothing
 end
 
-function update!(opt::Flux.Descent, tables::AbstractVector{<:HipEmbedding},
+function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  grads::AbstractVector{<:SparseEmbeddingUpdate},
                  indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
                  telemetry_cb = Returns(nothing), kw...) where {Nontemporal}
@@ -256,6 +306,6 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipEmbedding},
     return nothing
 end
 
-export HipEmbedding, HipArray, HipVector, HipMatrix, EmbtabError
+export HipEmbedding, HipSplitEmbedding, HipArray, HipVector, HipMatrix, EmbtabError
 
 end # module

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 1
+#define ET_ABI_VERSION 2
 
 /* Status codes. */
 #define ET_OK 0
@@ -111,6 +111,10 @@ typedef struct et_lookup_desc {
     int64_t ld_idx;      /* elements between consecutive bags' index lists */
     int64_t dst_row_off; /* first row of this table's block in dst (prependrows + sum of
                             previous tables' dims) */
+    int64_t cols_per_page; /* 0: contiguous table.  > 0: a PAGED table (the reference's
+                            SplitEmbedding, src/split.jl:3-86): `table` is a device array of
+                            page pointers, column r (1-based) lives in page (r-1)/cols_per_page
+                            at column (r-1)%cols_per_page, ld_table apart within a page */
 } et_lookup_desc;
 
 /* Fused lookup + concat (PreallocationStrategy):
@@ -138,6 +142,7 @@ typedef struct et_update_desc {
     const int64_t* idx;  /* the indices of the forward lookup (1-based) */
     int64_t ld_idx;
     int64_t batch;
+    int64_t cols_per_page; /* 0 or a paged table, as in et_lookup_desc */
 } et_update_desc;
 
 /* Bytes of device workspace needed by et_sparse_sgd for these descriptors. */
@@ -164,9 +169,10 @@ int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, doubl
  * src/sparseupdate.jl:436-544, where an IndexerView (src/utils.jl:320-338) selects a
  * range of distinct columns.  Every column's gradient is summed serially in `map`
  * order (exact).  `cumulative_*` and `map` are device arrays as written by
- * et_index_build; `eta` is the value the reference passes as `alpha`. */
-int et_update_indexed(int dtype, void* table, int64_t ld_table, int64_t nrows, int32_t dim,
-                      const void* delta, int64_t ld_delta, const int64_t* cumulative_col,
+ * et_index_build; `eta` is the value the reference passes as `alpha`;
+ * `cols_per_page` as in et_lookup_desc (0 = contiguous). */
+int et_update_indexed(int dtype, void* table, int64_t ld_table, int64_t cols_per_page,
+                      int64_t nrows, int32_t dim, const void* delta, int64_t ld_delta, const int64_t* cumulative_col,
                       const int64_t* cumulative_off, int64_t ubegin, int64_t uend,
                       const int64_t* map, double eta, uint32_t flags, void* stream);
 

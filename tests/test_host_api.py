@@ -66,3 +66,36 @@ def test_no_cpu_fallback():
     A = et.SimpleEmbedding(torch.rand(10, 16), et.Static(16))
     with pytest.raises(et.ArgumentError):
         et.lookup(A, torch.tensor([1, 2, 3]))
+
+
+def test_split_embedding_host_logic():
+    """src/split.jl:11-86: pages of cols_per_shard columns (last one short), Static{D},
+    size, columnpointer through _divrem_index, getindex/setindex!, undef constructor."""
+    data = torch.rand(23, 8)  # Julia 8 x 23
+    A = et.SplitEmbedding(data, 5)
+    assert [p.shape[0] for p in A.pages] == [5, 5, 5, 5, 3]
+    assert A.size() == (8, 23) and len(A) == 8 * 23
+    assert A.lookup_type == et.Static(8) and A.ld == 8 and A.cols_per_page == 5
+    assert torch.equal(A.to_dense(), data)
+    assert all(p.data_ptr() != data.data_ptr() for p in A.pages)  # copies, like the reference
+    # column 12 -> page 3, column 2 (1-based): _divrem_index(12, 5) == (3, 2)
+    assert A.columnpointer(12) == A.pages[2].data_ptr() + 1 * 8 * 4
+    assert A.columnpointer(23) == A.pages[4].data_ptr() + 2 * 8 * 4
+    with pytest.raises(IndexError):
+        A.columnpointer(26)
+    assert A[3, 12] == pytest.approx(float(data[11, 2]))
+    A[3, 12] = -7.0
+    assert float(A.pages[2][1, 2]) == -7.0
+    table, cpp = A.device_table()
+    assert table == A.page_table.data_ptr() and cpp == 5
+    assert A.page_table.tolist() == [p.data_ptr() for p in A.pages]
+    assert et.SimpleEmbedding(data).device_table() == (data.data_ptr(), 0)
+    U = et.SplitEmbedding.undef(16, 10, 4, torch.float32, "cpu", et.Dynamic)
+    assert U.size() == (16, 10) and U.lookup_type is et.Dynamic
+    assert [p.shape for p in U.pages] == [(4, 16), (4, 16), (2, 16)]
+    with pytest.raises(et.ArgumentError):
+        et.SplitEmbedding.undef(16, 10, 4, lookup_type=et.Static(8))
+    with pytest.raises(et.ArgumentError):
+        et.SplitEmbedding(data, 0)
+    with pytest.raises(et.ArgumentError):
+        et.lookup(A, torch.tensor([1, 2, 3]))  # no CPU fallback for paged tables either
