@@ -95,27 +95,40 @@ __device__ __forceinline__ long long load_idx_chunk(const int64_t* __restrict__ 
 // load is issued before the first add waits, so UU rows per group are in flight (the
 // waitcnt pass counts vmcnt down through the adds).  Row offsets use one 32x32->64
 // multiply (the host guarantees nrows and ld_table below 2^32).
-template <typename T, typename A, int D, int UU, bool NTL>
+//
+// PG (paged table, SplitEmbedding): `table` is the device array of page pointers and
+// column r lives in page r / cpp at column r % cpp; the UU page-pointer loads are
+// issued together before the row loads.
+template <typename T, typename A, int D, int UU, bool NTL, bool PG = false>
 __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t ld_table,
-                                         uint32_t nrows, long long my, int g, int sub, int i0,
-                                         bool first_batch,
+                                         uint32_t nrows, uint32_t cpp, long long my, int g,
+                                         int sub, int i0, bool first_batch,
                                          A (&acc)[VecGeom<T, D>::NV][VecGeom<T, D>::N],
                                          int& bad) {
     using G = VecGeom<T, D>;
     constexpr int N = G::N, LPR = G::LPR, NV = G::NV;
     uint64_t off[UU];
     bool ok[UU];
+    const T* base[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         const long long r = group_bcast<LPR>(my, i0 + u, g);
         const uint64_t row = (uint64_t)(r - 1);
         ok[u] = row < (uint64_t)nrows;
-        off[u] = ok[u] ? (uint64_t)(uint32_t)row * ld_table : 0;
+        const uint32_t row32 = ok[u] ? (uint32_t)row : 0u;
+        if constexpr (PG) {
+            const uint32_t page = row32 / cpp;
+            off[u] = (uint64_t)(row32 - page * cpp) * ld_table;
+            base[u] = reinterpret_cast<const T* const*>(table)[page];
+        } else {
+            off[u] = (uint64_t)row32 * ld_table;
+            base[u] = table;
+        }
     }
     u32x4 buf[UU][NV];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const u32x4* src = reinterpret_cast<const u32x4*>(table + off[u]) + sub;
+        const u32x4* src = reinterpret_cast<const u32x4*>(base[u] + off[u]) + sub;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if constexpr (NTL)
@@ -149,9 +162,10 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t l
 // Accumulation is acc = row(I[1]); acc += row(I[i]) for i = 2..P, element-wise and in
 // order (src/lookup.jl:139-146), so fp32/fp64/int results equal the reference bit
 // for bit; F16 rounds after every add (Julia Float16 `+`) unless A = float.
-template <typename T, typename A, int D, int U, bool NT, bool NTL>
+template <typename T, typename A, int D, int U, bool NT, bool NTL, bool PG = false>
 __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_t ld_table,
-                                            uint32_t nrows, const int64_t* __restrict__ ip,
+                                            uint32_t nrows, uint32_t cpp,
+                                            const int64_t* __restrict__ ip,
                                             int pool, long long my0, T* __restrict__ out, int g,
                                             int sub) {
     using G = VecGeom<T, D>;
@@ -167,33 +181,30 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_
         const int cnt = pool - c0 < LPR ? pool - c0 : LPR;
         const long long my = c0 == 0 ? my0 : load_idx_chunk<LPR>(ip + c0, cnt, sub);
         int i0 = 0;
-        for (; i0 + U <= cnt; i0 += U)
-            load_add<T, A, D, U, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0, acc,
-                                      bad);
+#define ET_LOAD_ADD(UU) \
+    load_add<T, A, D, UU, NTL, PG>(table, ld_table, nrows, cpp, my, g, sub, i0, c0 + i0 == 0, \
+                                   acc, bad)
+        for (; i0 + U <= cnt; i0 += U) ET_LOAD_ADD(U);
         if constexpr (U > 8) {
             if (cnt - i0 >= 8) {
-                load_add<T, A, D, 8, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0,
-                                          acc, bad);
+                ET_LOAD_ADD(8);
                 i0 += 8;
             }
         }
         if constexpr (U > 4) {
             if (cnt - i0 >= 4) {
-                load_add<T, A, D, 4, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0,
-                                          acc, bad);
+                ET_LOAD_ADD(4);
                 i0 += 4;
             }
         }
         if constexpr (U > 2) {
             if (cnt - i0 >= 2) {
-                load_add<T, A, D, 2, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0,
-                                          acc, bad);
+                ET_LOAD_ADD(2);
                 i0 += 2;
             }
         }
-        if (cnt - i0 >= 1)
-            load_add<T, A, D, 1, NTL>(table, ld_table, nrows, my, g, sub, i0, c0 + i0 == 0, acc,
-                                      bad);
+        if (cnt - i0 >= 1) ET_LOAD_ADD(1);
+#undef ET_LOAD_ADD
     }
     if (bad && sub == 0) note_oob(bad);
     u32x4* o = reinterpret_cast<u32x4*>(out) + sub;
@@ -208,7 +219,8 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_
 
 // `rounds` bags of one table per lane group, the next bag's first index chunk loaded
 // while the current bag's rows are in flight.
-template <typename T, typename A, int D, int U, bool NT, bool NTL, bool NTI = false>
+template <typename T, typename A, int D, int U, bool NT, bool NTL, bool NTI = false,
+          bool PG = false>
 __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
                                          T* __restrict__ dst, int64_t ld_dst, int64_t chunk,
                                          int rounds) {
@@ -230,21 +242,22 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
         if (r + 1 < rounds)
             my_next = load_idx_chunk<G::LPR, NTI>(
                 d.idx + (nbag < batch ? nbag : batch - 1) * d.ld_idx, cnt0, sub);
-        bag_sum_vec<T, A, D, U, NT, NTL>(table, ldt, nr, d.idx + bag * d.ld_idx, pool, my,
+        bag_sum_vec<T, A, D, U, NT, NTL, PG>(table, ldt, nr, (uint32_t)d.cols_per_page,
+                                             d.idx + bag * d.ld_idx, pool, my,
                                          dst + bag * ld_dst + d.dst_row_off, g, sub);
         bag = nbag;
     }
 }
 
 // Pooled-sum kernel, vector path: grid = ntables * nchunks workgroups of 256.
-template <typename T, typename A, int D, int U, bool NT>
+template <typename T, typename A, int D, int U, bool NT, bool PG = false>
 __global__ __launch_bounds__(256) void k_pooled_vec(LookupPack pack, int ntables, int64_t batch,
                                                     T* __restrict__ dst, int64_t ld_dst,
                                                     int rounds) {
     const int64_t item = blockIdx.x;
     const int t = (int)(item % ntables);
     const int64_t chunk = item / ntables;
-    run_bags<T, A, D, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    run_bags<T, A, D, U, NT, false, false, PG>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
 }
 
 // XCD-aware stripe schedule for multi-table launches.  Every table's chunks are cut
@@ -496,13 +509,16 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
     }
 }
 
-template <typename T, typename A, int D, int U, bool NT>
+template <typename T, typename A, int D, int U, bool NT, bool PG = false>
 int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                         hipStream_t s);
 
-template <typename T, typename A, int D, bool NT>
+template <typename T, typename A, int D, bool NT, bool PG = false>
 int launch_pooled_vec(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                       hipStream_t s) {
+    if constexpr (PG)  // paged tables: one schedule, the default rows in flight
+        return launch_pooled_vec_u<T, A, D, VecGeom<T, D>::U, NT, true>(pack, n, batch, dst,
+                                                                         ld_dst, s);
     if constexpr (D == 128 && __is_same(T, float)) {
         switch (tuning().rows_in_flight) {
             case 4: return launch_pooled_vec_u<T, A, D, 4, NT>(pack, n, batch, dst, ld_dst, s);
@@ -513,7 +529,7 @@ int launch_pooled_vec(const LookupPack& pack, int n, int64_t batch, void* dst, i
     return launch_pooled_vec_u<T, A, D, VecGeom<T, D>::U, NT>(pack, n, batch, dst, ld_dst, s);
 }
 
-template <typename T, typename A, int D, int U, bool NT>
+template <typename T, typename A, int D, int U, bool NT, bool PG>
 int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                         hipStream_t s) {
     using G = VecGeom<T, D>;
@@ -521,7 +537,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     const int rounds = rounds_for(batch, per_round, n);
     const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
     if (nchunks <= 0) return ET_OK;
-    if (n > 1 && tuning().striped) {
+    if (!PG && n > 1 && tuning().striped) {
         StripeMap sm;
         build_stripe_map(pack, n, (int)sizeof(T), sm);
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
@@ -541,8 +557,8 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     const int64_t grid = nchunks * n;
     if (grid <= 0) return ET_OK;
     if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
-    hipLaunchKernelGGL((k_pooled_vec<T, A, D, U, NT>), dim3((unsigned)grid), dim3(256), 0, s, pack,
-                       n, batch, reinterpret_cast<T*>(dst), ld_dst, rounds);
+    hipLaunchKernelGGL((k_pooled_vec<T, A, D, U, NT, PG>), dim3((unsigned)grid), dim3(256), 0, s,
+                       pack, n, batch, reinterpret_cast<T*>(dst), ld_dst, rounds);
     ET_LAUNCH_CHECK("k_pooled_vec");
     return ET_OK;
 }
@@ -582,16 +598,16 @@ int launch_gather(const LookupPack& pack, int n, int64_t rb, int64_t batch, void
     return fail(ET_ERR_UNSUPPORTED, "gather row bytes %lld", (long long)rb);
 }
 
-template <typename T, typename A, bool NT>
+template <typename T, typename A, bool NT, bool PG = false>
 int launch_pooled_dim(const LookupPack& pack, int n, int D, int64_t batch, void* dst,
                       int64_t ld_dst, hipStream_t s) {
     switch (D) {
-        case 16: return launch_pooled_vec<T, A, 16, NT>(pack, n, batch, dst, ld_dst, s);
-        case 32: return launch_pooled_vec<T, A, 32, NT>(pack, n, batch, dst, ld_dst, s);
-        case 64: return launch_pooled_vec<T, A, 64, NT>(pack, n, batch, dst, ld_dst, s);
-        case 128: return launch_pooled_vec<T, A, 128, NT>(pack, n, batch, dst, ld_dst, s);
-        case 256: return launch_pooled_vec<T, A, 256, NT>(pack, n, batch, dst, ld_dst, s);
-        case 512: return launch_pooled_vec<T, A, 512, NT>(pack, n, batch, dst, ld_dst, s);
+        case 16: return launch_pooled_vec<T, A, 16, NT, PG>(pack, n, batch, dst, ld_dst, s);
+        case 32: return launch_pooled_vec<T, A, 32, NT, PG>(pack, n, batch, dst, ld_dst, s);
+        case 64: return launch_pooled_vec<T, A, 64, NT, PG>(pack, n, batch, dst, ld_dst, s);
+        case 128: return launch_pooled_vec<T, A, 128, NT, PG>(pack, n, batch, dst, ld_dst, s);
+        case 256: return launch_pooled_vec<T, A, 256, NT, PG>(pack, n, batch, dst, ld_dst, s);
+        case 512: return launch_pooled_vec<T, A, 512, NT, PG>(pack, n, batch, dst, ld_dst, s);
     }
     return fail(ET_ERR_UNSUPPORTED, "vector dim %d", D);
 }
@@ -609,7 +625,7 @@ int launch_generic(const LookupPack& pack, int n, int64_t batch, void* dst, int6
 }
 
 // Kinds of launch group.
-enum GroupKind { kGather = 0, kPooledVec = 1, kGeneric = 2 };
+enum GroupKind { kGather = 0, kPooledVec = 1, kGeneric = 2, kPagedVec = 3 };
 
 template <typename T, typename A, bool NT>
 int launch_group_typed(GroupKind kind, const LookupPack& pack, int n, int D, int64_t batch,
@@ -618,6 +634,8 @@ int launch_group_typed(GroupKind kind, const LookupPack& pack, int n, int D, int
     if (kind == kGather)
         return launch_gather<NT>(pack, n, (int64_t)D * es, batch, dst, ld_dst, es, s);
     if (kind == kPooledVec) return launch_pooled_dim<T, A, NT>(pack, n, D, batch, dst, ld_dst, s);
+    if (kind == kPagedVec)
+        return launch_pooled_dim<T, A, NT, true>(pack, n, D, batch, dst, ld_dst, s);
     return launch_generic<T, A, NT>(pack, n, batch, dst, ld_dst, s);
 }
 
@@ -686,7 +704,12 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
         if (d.dim == 0) {
             kind_of[t] = -1;
         } else if (d.cols_per_page != 0) {
-            kind_of[t] = kGeneric;  // paged (SplitEmbedding) tables: layout-agnostic kernel
+            // paged (SplitEmbedding) table: the pooled vector kernel with page addressing
+            // (a non-reducing lookup is its pool = 1 case, still a bit copy); pages are
+            // 16-byte aligned by contract (include/embtab.h)
+            const bool vec = d.pool >= 1 && al && vec_dim_ok(d.dim) && d.nrows < 0xffffffffll &&
+                             d.ld_table < 0xffffffffll && d.cols_per_page < 0xffffffffll;
+            kind_of[t] = vec ? kPagedVec : kGeneric;
         } else if (d.pool == 1 && al && gather_rb_ok((int64_t)d.dim * es)) {
             kind_of[t] = kGather;
         } else if (d.pool >= 1 && al && vec_dim_ok(d.dim) && d.nrows < 0xffffffffll &&

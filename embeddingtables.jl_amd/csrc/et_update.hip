@@ -285,8 +285,8 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
             const int t = table_of_key(pack, ntables, kkey);
             const et_update_desc& d = pack.d[t];
             if (!((pack.vec_mask >> t) & 1u)) continue;  // the generic kernels' table
-            float* w = reinterpret_cast<float*>(d.table) +
-                       (uint64_t)(kkey - pack.row_off[t]) * (uint64_t)d.ld_table;
+            float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
+                                      kkey - pack.row_off[t]);
             u32x4 x[NV];
             if (dsl == 0xffffffffu) {
                 const u32x4* wp = reinterpret_cast<const u32x4*>(w) + sub;
@@ -390,8 +390,8 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
                 const uint32_t key = keys[seg_start[seg]];
                 const int t = table_of_key(pack, ntables, key);
                 const et_update_desc& d = pack.d[t];
-                float* w = reinterpret_cast<float*>(d.table) +
-                           (uint64_t)(key - pack.row_off[t]) * (uint64_t)d.ld_table;
+                float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
+                                          key - pack.row_off[t]);
                 u32x4 x[NV];
                 const u32x4* wp = reinterpret_cast<const u32x4*>(w) + sub;
 #pragma unroll
@@ -691,7 +691,8 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         ro += (uint32_t)d.nrows;
         oo += (uint32_t)(d.pool * d.batch);
         if (d.pool == 0 || d.batch == 0 || d.dim == 0) continue;
-        const bool vec_ok = d.cols_per_page == 0 && et::aligned16(d.table) &&
+        // paged tables qualify too: their pages are 16-byte aligned by contract
+        const bool vec_ok = (d.cols_per_page > 0 || et::aligned16(d.table)) &&
                             et::aligned16(d.delta) && (d.ld_table % 4 == 0) &&
                             (d.ld_delta % 4 == 0) && et::vec_dim_ok(d.dim) &&
                             (vec_dim < 0 || vec_dim == d.dim);

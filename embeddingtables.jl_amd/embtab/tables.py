@@ -230,6 +230,8 @@ class SplitEmbedding(AbstractEmbeddingTable):
     def _init(self, pages, D, cps, dtype, device):
         if not pages:
             raise ArgumentError("a SplitEmbedding needs at least one column")
+        if any(p.data_ptr() % 16 for p in pages):
+            raise ArgumentError("every page must be 16-byte aligned (include/embtab.h)")
         self.pages = pages
         self.matrixsize = (D, cps)
         self.lookup_type = Static(D)

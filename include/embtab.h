@@ -114,7 +114,8 @@ typedef struct et_lookup_desc {
     int64_t cols_per_page; /* 0: contiguous table.  > 0: a PAGED table (the reference's
                             SplitEmbedding, src/split.jl:3-86): `table` is a device array of
                             page pointers, column r (1-based) lives in page (r-1)/cols_per_page
-                            at column (r-1)%cols_per_page, ld_table apart within a page */
+                            at column (r-1)%cols_per_page, ld_table apart within a page;
+                            every page pointer must be 16-byte aligned (hipMalloc gives 256) */
 } et_lookup_desc;
 
 /* Fused lookup + concat (PreallocationStrategy):
