@@ -37,10 +37,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 TABLE_SEED, INDEX_SEED = 1000, 2000
 
 
-def algorithmic_bytes(batch, ntables, pool, dims, es=4):
+def algorithmic_bytes(batch, pool, dims, es=4):
     """Per launch: every gathered row + every index + every output element
-    (SURVEY.md §8d)."""
-    return batch * ntables * pool * DIM * es + batch * ntables * pool * 8 + batch * sum(dims) * es
+    (SURVEY.md §8d), summed over the tables (or table pieces) of the launch."""
+    return sum(batch * pool * d * es + batch * pool * 8 + batch * d * es for d in dims)
 
 
 def parse():
@@ -57,6 +57,12 @@ def parse():
                    help="skip the config-2 (gather) and config-4 (Zipf + SGD) measurements")
     p.add_argument("--force-shard", action="store_true",
                    help="use the sharded (all-gather + concat) step even on one rank")
+    p.add_argument("--plan", choices=["featurewise", "tablewise"], default="featurewise",
+                   help="N > 1: equal feature ranges (default) or whole tables per rank")
+    p.add_argument("--chunks", type=int, default=4,
+                   help="N > 1: batch chunks pipelined through lookup / all-gather / concat")
+    p.add_argument("--no-alltoall", action="store_true",
+                   help="N > 1: skip the extra all-to-all (batch-sliced output) measurement")
     p.add_argument("--subset", choices=["all", "heavy", "light"], default="all",
                    help="calibration only: tables above / below 4 MiB")
     p.add_argument("--rows", type=int, default=0,
@@ -178,6 +184,31 @@ def bench_config2(et, L, device, steps, warmup):
             "algorithmic_bytes_per_launch": nbytes, "bit_identical": ok}
 
 
+def bench_alltoall(plan, rank, world, B, device, tables, idx, steps, warmup):
+    """The DLRM layout: same lookups, but rank r keeps only its
+    batch slice of the destination (RCCL all-to-all instead of all-gather)."""
+    import torch
+    import torch.distributed as dist
+    from embtab.sharding import ShardedMapLookup
+
+    a2a = ShardedMapLookup(plan, rank, world, B, torch.float32, device, exchange="alltoall")
+    out = torch.empty((a2a.mine, plan.ld), dtype=torch.float32, device=device)
+    for _ in range(warmup):
+        a2a(tables, idx, out)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        a2a(tables, idx, out)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ms = 1e3 * float(el.item()) / steps
+    return {"ms_per_step": ms, "value": B * len(plan.dims) * POOL / (ms * 1e-3),
+            "unit": "lookups/s", "output": "batch slice per rank"}
+
+
 def zipf_indices(R, shape, alpha, gen, device):
     """Bounded Zipf(alpha) ranks over 1..R by the continuous inverse CDF, mapped through
     a seeded random permutation of the table."""
@@ -254,7 +285,7 @@ def main():
 
     import embtab as et
     from embtab import _lib
-    from embtab.sharding import ShardLayout, ShardedPreallocation, plan_tables
+    from embtab.sharding import ShardedMapLookup, ShardPlan, piece_table
 
     if args.rows:
         CRITEO_KAGGLE_ROWS[:] = [args.rows] * len(CRITEO_KAGGLE_ROWS)
@@ -275,28 +306,39 @@ def main():
         CRITEO_KAGGLE_ROWS[:] = keep
     T = len(CRITEO_KAGGLE_ROWS)
     dims = [DIM] * T
-    assignment = plan_tables(T, world)
-    mine = assignment[rank]
-    tables = make_tables(et, L, mine, device)
-    idx = make_indices(L, mine, B, device)
-    layout = ShardLayout(dims, 0, assignment)
-    dst = torch.empty((B, layout.ld), dtype=torch.float32, device=device)
+    sharded = world > 1 or args.force_shard
+    if sharded:
+        plan = (ShardPlan.featurewise(dims, world) if args.plan == "featurewise"
+                else ShardPlan.tablewise(dims, world))
+        mine = plan.tables_of(rank)
+        full = dict(zip(mine, make_tables(et, L, mine, device)))
+        fidx = dict(zip(mine, make_indices(L, mine, B, device)))
+        pieces = plan.pieces[rank]
+        tables = [piece_table(full[p.table], p) for p in pieces]
+        idx = [fidx[p.table] for p in pieces]
+        local_dims = [p.dim for p in pieces]
+        shard = ShardedMapLookup(plan, rank, world, B, torch.float32, device,
+                                 exchange="allgather", chunks=args.chunks)
+    else:
+        mine = list(range(T))
+        tables = make_tables(et, L, mine, device)
+        idx = make_indices(L, mine, B, device)
+        local_dims = dims
+    dst = torch.empty((B, sum(dims)), dtype=torch.float32, device=device)
     strat = et.PreallocationStrategy(0)
-    sharded = ShardedPreallocation(layout, rank, world, B, torch.float32, device) \
-        if world > 1 or args.force_shard else None
 
     def step():
-        if sharded is None:
-            et.maplookup_(strat, dst, tables, idx)
+        if sharded:
+            shard(tables, idx, dst)
         else:
-            sharded(tables, idx, dst)
+            et.maplookup_(strat, dst, tables, idx)
 
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    # kernel-level timing of the dominant launch on the stream it runs on
+    # kernel-level timing of the dominant launch(es) on the stream they run on
     stream = torch.cuda.current_stream(device)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -305,16 +347,12 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        if sharded is None:
-            ev[k][0].record(stream)
-            et.maplookup_(strat, dst, tables, idx)
-            ev[k][1].record(stream)
+        ev[k][0].record(stream)
+        if sharded:
+            shard(tables, idx, dst)  # lookups on `stream`, exchange on a second stream
         else:
-            ev[k][0].record(stream)
-            sharded.local_lookup(tables, idx)
-            ev[k][1].record(stream)
-            sharded.exchange()
-            sharded.assemble(dst)
+            et.maplookup_(strat, dst, tables, idx)
+        ev[k][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -323,11 +361,19 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if sharded:  # lookup-only time: the chunked lookups alone, same launches, no exchange
+        torch.cuda.synchronize()
+        for k in range(args.steps):
+            ev[k][0].record(stream)
+            for c in range(shard.chunks):
+                shard.lookup_chunk(tables, idx, shard.bounds[c], shard.bounds[c + 1])
+            ev[k][1].record(stream)
+        torch.cuda.synchronize()
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
     lookups_per_step = B * T * POOL
     value = lookups_per_step * args.steps / elapsed
-    local_bytes = algorithmic_bytes(B, len(mine), POOL, [DIM] * len(mine))
+    local_bytes = algorithmic_bytes(B, POOL, local_dims)
     achieved = local_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = load_traffic()
     traffic_bytes = None
@@ -357,7 +403,8 @@ def main():
             "pool": POOL,
             "dim": DIM,
             "table_rows": CRITEO_KAGGLE_ROWS,
-            "parallelism": "single GPU" if world == 1 else f"table-wise x{world} + RCCL all-gather",
+            "parallelism": "single GPU" if not sharded else
+                           f"{args.plan} x{world} + RCCL all-gather ({shard.chunks} chunks)",
         },
         "bags_per_s": B * T * args.steps / elapsed,
         "samples_per_s": B * args.steps / elapsed,
@@ -373,8 +420,12 @@ def main():
             "kernel_ms": kernel_ms,
         },
     }
-    if sharded is not None:
+    if sharded:
         result["lookup_only_ms"] = kernel_ms
+        result["slab_cols"] = plan.slab_ld
+        if world > 1 and not args.no_alltoall:
+            result["alltoall"] = bench_alltoall(plan, rank, world, B, device, tables, idx,
+                                                max(5, args.steps // 2), 2)
     if world == 1 and not args.no_extra:
         result["config2_gather"] = bench_config2(et, L, device, 50, 5)
         result["config4_zipf_update"] = bench_config4(et, tables, mine, device, 10, 2, B)

@@ -1,24 +1,41 @@
-"""Table-wise sharding of a PreallocationStrategy maplookup across the GPUs of a node.
+"""Sharding a PreallocationStrategy maplookup across the GPUs of a node.
 
-No counterpart exists in the single-process reference: tables
-are independent, so each rank owns whole tables, looks them up for the full batch
-into a local slab with ONE fused launch, and the concat of the reference's
-PreallocationStrategy (src/lookup.jl:334-340) becomes an RCCL all-gather of the
-slabs over xGMI plus one assembly kernel (et_concat_slabs) into the
-``(B, prependrows + sum D)`` destination.
+No counterpart exists in the single-process reference.  Tables
+are independent, and so is every feature of a table (a pooled sum is computed
+feature by feature, src/lookup.jl:134-147), so a rank can own any set of
+*pieces* — a table, or a contiguous feature range of one — look them up for the
+batch with ONE fused launch per feature-width group into a local slab, and the
+concat of the reference's PreallocationStrategy (src/lookup.jl:334-340) becomes
+an RCCL exchange of the slabs over xGMI plus one assembly kernel
+(et_concat_slabs) into the destination.
 
-The data path is: et_maplookup_prealloc (local tables -> slab) ->
-all_gather_into_tensor (slabs, RCCL) -> et_concat_slabs (slabs -> dst).
+Plans:
+  * ``ShardPlan.tablewise``: whole tables, balanced by count (4,4,3,3,3,3,3,3 for
+    26 tables on 8 GPUs);
+  * ``ShardPlan.featurewise``: the concatenated feature axis cut into equal
+    contiguous ranges at ``granule``-feature boundaries (26 x 128 = 3328 features
+    -> 416 per GPU at N = 8): equal slabs (no all-gather padding) and equal
+    lookup bytes per rank.  Results are bit-identical to the unsharded lookup.
+
+Exchanges:
+  * ``"allgather"`` (the contract, BASELINE config 5): every rank ends with the
+    whole ``(B, k + sum D)`` destination; the batch is cut into ``chunks`` so the
+    lookup of chunk c+1 overlaps the all-gather + assembly of chunk c on a second
+    stream;
+  * ``"alltoall"`` (the DLRM layout): rank r ends with rows
+    ``[r*B/N, (r+1)*B/N)`` of the destination — N times less data on the links.
 """
 from __future__ import annotations
 
 import ctypes
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import torch
 
 from . import _lib
 from .lookup import _ld
+
+VEC_DIMS = (512, 256, 128, 64, 32, 16)  # the vector kernels' feature widths
 
 
 def plan_tables(ntables: int, world: int, sizes=None) -> list[list[int]]:
@@ -48,113 +65,263 @@ def plan_tables(ntables: int, world: int, sizes=None) -> list[list[int]]:
     return [sorted(o) for o in out]
 
 
-@dataclass
-class ShardLayout:
-    """Where every rank's tables land in the concat destination."""
+@dataclass(frozen=True)
+class Piece:
+    """Features ``[f0, f0 + dim)`` of global table ``table``; its columns of the
+    destination start at ``col`` (prependrows included)."""
 
-    dims: list[int]
-    prependrows: int
-    assignment: list[list[int]]
-    offsets: list[int] = field(init=False)  # dst row of each global table
-    rank_rows: list[int] = field(init=False)
-    slab_ld: int = field(init=False)
+    table: int
+    f0: int
+    dim: int
+    col: int
 
-    def __post_init__(self):
-        off = self.prependrows
-        self.offsets = []
-        for d in self.dims:
-            self.offsets.append(off)
-            off += d
-        self.ld = off
-        self.rank_rows = [sum(self.dims[t] for t in ts) for ts in self.assignment]
-        # pad the slab to a multiple of 4 elements so 16-B vector stores stay aligned
-        self.slab_ld = max(4, (max(self.rank_rows) + 3) // 4 * 4)
 
-    def rank_segments(self, r: int):
-        """Contiguous (slab_row, dst_row, rows) runs of rank r's tables."""
-        segs = []
-        srow = 0
-        for t in self.assignment[r]:
-            d = self.dims[t]
-            if segs and segs[-1][1] + segs[-1][2] == self.offsets[t] and \
-                    segs[-1][0] + segs[-1][2] == srow:
-                segs[-1] = (segs[-1][0], segs[-1][1], segs[-1][2] + d)
+def _vec_split(t: int, f0: int, dim: int, col: int, es: int = 4) -> list[Piece]:
+    """Cut a feature range into vector-kernel widths where alignment allows (96 ->
+    64 + 32); anything else stays one piece (the generic kernel takes it)."""
+    out = []
+    while dim > 0:
+        w = next((v for v in VEC_DIMS if v <= dim and (f0 * es) % 16 == 0), None)
+        if w is None or (dim not in VEC_DIMS and dim % 16 != 0):
+            out.append(Piece(t, f0, dim, col))
+            break
+        out.append(Piece(t, f0, w, col))
+        f0, dim, col = f0 + w, dim - w, col + w
+    return out
+
+
+def plan_features(dims, world: int, granule: int = 32) -> list[tuple[int, int]]:
+    """Feature ranges ``[lo, hi)`` of the concatenated feature axis, one per rank:
+    cut points are table edges or multiples of ``granule`` inside a table, each
+    chosen nearest to an equal split."""
+    if world <= 0:
+        raise ValueError("world must be positive")
+    cuts, start = {0}, 0
+    for d in dims:
+        for f in range(granule, d, granule):
+            cuts.add(start + f)
+        start += d
+        cuts.add(start)
+    F = start
+    cands = sorted(cuts)
+    bounds = [0]
+    for r in range(1, world):
+        target = F * r / world
+        best = min((c for c in cands if c >= bounds[-1]), key=lambda c: (abs(c - target), c))
+        bounds.append(best)
+    bounds.append(F)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+class ShardPlan:
+    """Which pieces every rank looks up, and where its slab lands in the destination."""
+
+    def __init__(self, dims, prependrows: int, pieces: list[list[Piece]]):
+        self.dims = list(dims)
+        self.prependrows = prependrows
+        self.pieces = pieces
+        self.world = len(pieces)
+        self.ld = prependrows + sum(self.dims)
+        self.widths = [sum(p.dim for p in ps) for ps in pieces]
+        # equal slabs for the collective; a multiple of 4 elements keeps 16-B stores aligned
+        self.slab_ld = max(4, (max(self.widths) + 3) // 4 * 4)
+
+    @classmethod
+    def tablewise(cls, dims, world: int, prependrows: int = 0, sizes=None) -> "ShardPlan":
+        offs = _table_cols(dims, prependrows)
+        return cls(dims, prependrows,
+                   [[Piece(t, 0, dims[t], offs[t]) for t in ts]
+                    for ts in plan_tables(len(dims), world, sizes)])
+
+    @classmethod
+    def featurewise(cls, dims, world: int, prependrows: int = 0,
+                    granule: int = 32) -> "ShardPlan":
+        offs = _table_cols(dims, prependrows)
+        starts = [o - prependrows for o in offs]
+        pieces = []
+        for lo, hi in plan_features(dims, world, granule):
+            mine = []
+            for t, d in enumerate(dims):
+                a, b = max(lo, starts[t]), min(hi, starts[t] + d)
+                if a < b:
+                    mine += _vec_split(t, a - starts[t], b - a, prependrows + a)
+            pieces.append(mine)
+        return cls(dims, prependrows, pieces)
+
+    def tables_of(self, rank: int) -> list[int]:
+        """Global ids of the tables rank ``rank`` reads (each once, in order)."""
+        seen = []
+        for p in self.pieces[rank]:
+            if p.table not in seen:
+                seen.append(p.table)
+        return seen
+
+    def runs(self, rank: int):
+        """Contiguous ``(slab_col, dst_col, ncols)`` runs of a rank's slab."""
+        runs, s = [], 0
+        for p in self.pieces[rank]:
+            if runs and runs[-1][0] + runs[-1][2] == s and runs[-1][1] + runs[-1][2] == p.col:
+                runs[-1] = (runs[-1][0], runs[-1][1], runs[-1][2] + p.dim)
             else:
-                segs.append((srow, self.offsets[t], d))
-            srow += d
-        return segs
-
-
-class ShardedPreallocation:
-    """maplookup(PreallocationStrategy(k), tables, I) with the tables split over ranks.
-
-    ``local_tables`` / ``local_idx`` are this rank's tables (in assignment order) and
-    their index arrays.  ``group`` is a torch.distributed process group (RCCL on
-    ROCm)."""
-
-    def __init__(self, layout: ShardLayout, rank: int, world: int, batch: int, dtype, device,
-                 group=None):
-        self.layout, self.rank, self.world, self.batch = layout, rank, world, batch
-        self.device = device
-        self.group = group
-        self.slab = torch.empty((batch, layout.slab_ld), dtype=dtype, device=device)
-        self.gathered = torch.empty((world, batch, layout.slab_ld), dtype=dtype, device=device)
-        # Per-rank contiguous segments -> et_concat_slabs requires one run per rank, so
-        # assignments are contiguous table ranges (plan_tables without sizes) or the
-        # concat is issued once per run.
-        self.runs = [layout.rank_segments(r) for r in range(world)]
-
-    def local_lookup(self, local_tables, local_idx, nontemporal=True):
-        """One fused launch: this rank's tables -> its slab."""
-        from .lookup import PreallocationStrategy, maplookup_
-
-        maplookup_(PreallocationStrategy(0), self.slab, local_tables, local_idx, nontemporal)
-        return self.slab
-
-    def exchange(self):
-        import torch.distributed as dist
-
-        if self.world == 1:
-            self.gathered[0].copy_(self.slab)
-            return self.gathered
-        if dist.get_backend(self.group) == "gloo":  # CPU rehearsal: no all_gather_into_tensor
-            dist.all_gather(list(self.gathered.unbind(0)), self.slab, group=self.group)
-        else:
-            dist.all_gather_into_tensor(self.gathered.view(-1), self.slab.view(-1),
-                                        group=self.group)
-        return self.gathered
+                runs.append((s, p.col, p.dim))
+            s += p.dim
+        return runs
 
     def assembly_launches(self):
-        """The et_concat_slabs launches that assemble the destination: a list of
-        ``(slab_row_shift, rows[rank], dst_row_off[rank])``.  With contiguous table
-        ranges per rank (plan_tables without sizes) this is one launch."""
+        """The et_concat_slabs launches that assemble the destination from the
+        gathered slabs: ``(slab_col_shift, ncols[rank], dst_col[rank])`` — one launch
+        when every rank's pieces are one contiguous run (featurewise, or tablewise
+        without ``sizes``)."""
+        all_runs = [self.runs(r) for r in range(self.world)]
         launches = []
-        max_runs = max(len(r) for r in self.runs)
-        for k in range(max_runs):
+        for k in range(max((len(x) for x in all_runs), default=0)):
             per = {}
             for r in range(self.world):
-                if k < len(self.runs[r]):
-                    srow, drow, n = self.runs[r][k]
-                    rows, offs = per.setdefault(srow, ([0] * self.world, [0] * self.world))
-                    rows[r], offs[r] = n, drow
+                if k < len(all_runs[r]):
+                    s, d, n = all_runs[r][k]
+                    rows, offs = per.setdefault(s, ([0] * self.world, [0] * self.world))
+                    rows[r], offs[r] = n, d
             for shift in sorted(per):
                 launches.append((shift, per[shift][0], per[shift][1]))
         return launches
 
-    def assemble(self, dst: torch.Tensor):
-        """et_concat_slabs: every rank's slab rows into their dst rows."""
+
+def _table_cols(dims, prependrows):
+    offs, c = [], prependrows
+    for d in dims:
+        offs.append(c)
+        c += d
+    return offs
+
+
+def piece_table(full, piece: Piece):
+    """A rank's view of ``piece`` of a full table (a SimpleEmbedding on a column
+    slice; whole-table pieces return the table itself).  The view keeps the
+    reference's update dispatch of the parent (fused iff the parent is)."""
+    from .tables import Dynamic, SimpleEmbedding, Static, fused_update_path
+
+    D = full.size()[0]
+    if piece.f0 == 0 and piece.dim == D:
+        return full
+    if not isinstance(full, SimpleEmbedding):
+        raise NotImplementedError("feature-sharding needs SimpleEmbedding tables")
+    view = full.data[:, piece.f0:piece.f0 + piece.dim]
+    return SimpleEmbedding(view, Static(piece.dim) if fused_update_path(full) else Dynamic)
+
+
+class ShardedMapLookup:
+    """``maplookup!(PreallocationStrategy(k), dst, tables, I)`` over the ranks of
+    ``group`` (RCCL on ROCm; gloo for CPU rehearsal).
+
+    ``piece_tables`` / ``piece_idx`` are this rank's pieces (``piece_table``) and
+    their index arrays, in ``plan.pieces[rank]`` order."""
+
+    def __init__(self, plan: ShardPlan, rank: int, world: int, batch: int, dtype, device,
+                 group=None, exchange: str = "allgather", chunks: int = 1):
+        if plan.world != world:
+            raise ValueError("plan and world size differ")
+        if exchange not in ("allgather", "alltoall"):
+            raise ValueError(f"unknown exchange {exchange!r}")
+        self.plan, self.rank, self.world, self.batch = plan, rank, world, batch
+        self.device, self.group, self.exchange_kind = torch.device(device), group, exchange
+        self.chunks = max(1, min(chunks, batch)) if exchange == "allgather" else 1
+        ld = plan.slab_ld
+        self.slab = torch.zeros((batch, ld), dtype=dtype, device=device)
+        # chunk c covers batch rows [bounds[c], bounds[c+1])
+        self.bounds = [batch * c // self.chunks for c in range(self.chunks + 1)]
+        if exchange == "allgather":
+            self.gathered = [torch.empty((world, self.bounds[c + 1] - self.bounds[c], ld),
+                                         dtype=dtype, device=device)
+                             for c in range(self.chunks)]
+        else:
+            # rank j receives batch rows [split[j], split[j+1]) from every rank
+            self.split = [batch * j // world for j in range(world + 1)]
+            self.mine = self.split[rank + 1] - self.split[rank]
+            self.gathered = [torch.empty((world, self.mine, ld), dtype=dtype, device=device)]
+        self.launches = plan.assembly_launches()
+        self._comm = (torch.cuda.Stream(self.device) if self.device.type == "cuda"
+                      and self.chunks > 1 else None)
+        self._events = []
+
+    # --- device work (overridable so that the CPU rehearsal can stand in the oracle) ---
+    def lookup_chunk(self, piece_tables, piece_idx, b0: int, b1: int):
+        """One fused launch per width group: this rank's pieces, bags [b0, b1) -> slab."""
+        from .lookup import PreallocationStrategy, maplookup_
+
+        if piece_tables:
+            maplookup_(PreallocationStrategy(0), self.slab[b0:b1], piece_tables,
+                       [i[b0:b1] for i in piece_idx])
+
+    def assemble_chunk(self, gathered: torch.Tensor, dst: torch.Tensor):
+        """et_concat_slabs: every rank's slab columns into their destination columns."""
         L = _lib.load()
-        for shift, rows, offs in self.assembly_launches():
+        nb = gathered.shape[1]
+        for shift, rows, offs in self.launches:
             rr = (ctypes.c_int32 * self.world)(*rows)
             oo = (ctypes.c_int64 * self.world)(*offs)
-            base = self.gathered.data_ptr() + shift * self.gathered.element_size()
+            base = gathered.data_ptr() + shift * gathered.element_size()
             _lib.check(L.et_concat_slabs(
-                _lib.et_dtype(dst), base, self.world, self.layout.slab_ld, self.batch,
+                _lib.et_dtype(dst), base, self.world, self.plan.slab_ld, nb,
                 ctypes.addressof(rr), ctypes.addressof(oo), dst.data_ptr(), _ld(dst),
                 _lib.stream_handle(dst.device)))
+
+    # --- the exchange -------------------------------------------------------------------
+    def _all_gather(self, out: torch.Tensor, inp: torch.Tensor):
+        import torch.distributed as dist
+
+        if self.world == 1:
+            out[0].copy_(inp)
+        elif dist.get_backend(self.group) == "gloo":  # no all_gather_into_tensor on gloo
+            dist.all_gather(list(out.unbind(0)), inp.contiguous(), group=self.group)
+        else:
+            dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=self.group)
+
+    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor):
+        import torch.distributed as dist
+
+        if self.world == 1:
+            out[0].copy_(inp)
+            return
+        sizes_in = [(self.split[j + 1] - self.split[j]) * self.plan.slab_ld
+                    for j in range(self.world)]
+        dist.all_to_all_single(out.view(-1), inp.reshape(-1),
+                               output_split_sizes=[self.mine * self.plan.slab_ld] * self.world,
+                               input_split_sizes=sizes_in, group=self.group)
+
+    def __call__(self, piece_tables, piece_idx, dst: torch.Tensor) -> torch.Tensor:
+        """Run the sharded step; ``dst`` is ``(B, k + sum D)`` (allgather) or this
+        rank's ``(B_r, k + sum D)`` batch slice (alltoall)."""
+        if self.exchange_kind == "alltoall":
+            self.lookup_chunk(piece_tables, piece_idx, 0, self.batch)
+            self._all_to_all(self.gathered[0], self.slab)
+            self.assemble_chunk(self.gathered[0], dst)
+            return dst
+        if self._comm is None:
+            for c in range(self.chunks):
+                b0, b1 = self.bounds[c], self.bounds[c + 1]
+                self.lookup_chunk(piece_tables, piece_idx, b0, b1)
+                self._all_gather(self.gathered[c], self.slab[b0:b1])
+                self.assemble_chunk(self.gathered[c], dst[b0:b1])
+            return dst
+        # pipelined: lookups on the caller's stream, exchange + assembly on _comm
+        main = torch.cuda.current_stream(self.device)
+        self._comm.wait_stream(main)  # dst / slab reuse across steps
+        for c in range(self.chunks):
+            b0, b1 = self.bounds[c], self.bounds[c + 1]
+            self.lookup_chunk(piece_tables, piece_idx, b0, b1)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self._comm.wait_event(ev)
+            with torch.cuda.stream(self._comm):
+                self._all_gather(self.gathered[c], self.slab[b0:b1])
+                self.assemble_chunk(self.gathered[c], dst[b0:b1])
+        main.wait_stream(self._comm)
         return dst
 
-    def __call__(self, local_tables, local_idx, dst: torch.Tensor):
-        self.local_lookup(local_tables, local_idx)
-        self.exchange()
-        return self.assemble(dst)
+
+class ShardedPreallocation(ShardedMapLookup):
+    """Round-1 name: table-wise plan, all-gather exchange, one chunk."""
+
+    def __init__(self, plan: ShardPlan, rank: int, world: int, batch: int, dtype, device,
+                 group=None):
+        super().__init__(plan, rank, world, batch, dtype, device, group, "allgather", 1)

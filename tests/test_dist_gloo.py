@@ -1,7 +1,8 @@
-"""Table-wise sharded Preallocation maplookup on 2 CPU ranks (gloo): the real
-plan / layout / all-gather / assembly-plan code of embtab.sharding, with the oracle
-standing in for the two device kernels (et_maplookup_prealloc into the slab and
-et_concat_slabs), checked against the single-process Preallocation result."""
+"""Sharded Preallocation maplookup on 2 and 3 CPU ranks (gloo): the real plans,
+piece decomposition, chunked all-gather / all-to-all exchange and assembly plan of
+embtab.sharding, with the oracle standing in for the two device kernels
+(et_maplookup_prealloc into the slab and et_concat_slabs), checked against the
+single-process Preallocation result."""
 import os
 import socket
 
@@ -11,28 +12,43 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from embtab.sharding import ShardLayout, ShardedPreallocation, plan_tables
+from embtab.sharding import ShardedMapLookup, ShardPlan, plan_features, plan_tables
+
+CRITEO = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194,
+          27, 14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572]
 
 
 def test_plan_tables_counts():
     a = plan_tables(26, 8)
     assert [len(x) for x in a] == [4, 4, 3, 3, 3, 3, 3, 3]
     assert sorted(t for x in a for t in x) == list(range(26))
-    rows = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593, 3194,
-            27, 14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105, 142572]
-    b = plan_tables(26, 8, sizes=rows)
-    big5 = sorted(range(26), key=lambda t: -rows[t])[:5]
+    b = plan_tables(26, 8, sizes=CRITEO)
+    big5 = sorted(range(26), key=lambda t: -CRITEO[t])[:5]
     owners = [next(r for r, x in enumerate(b) if t in x) for t in big5]
     assert len(set(owners)) == 5  # the five largest tables on distinct GPUs
     assert [len(x) for x in b] == [4, 4, 3, 3, 3, 3, 3, 3]
     assert plan_tables(26, 2) == [list(range(13)), list(range(13, 26))]
 
 
-def _concat_numpy(gathered, slab_ld, shift, rows, offs, dst):
-    """et_concat_slabs semantics (include/embtab.h) on host arrays."""
-    for r, (n, o) in enumerate(zip(rows, offs)):
-        if n:
-            dst[:, o:o + n] = gathered[r][:, shift:shift + n]
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_featurewise_plan_covers_every_feature_once(world):
+    dims = [128] * 26
+    plan = ShardPlan.featurewise(dims, world, prependrows=16)
+    seen = np.zeros((26, 128), np.int32)
+    for r, ps in enumerate(plan.pieces):
+        col = None
+        for p in ps:
+            seen[p.table, p.f0:p.f0 + p.dim] += 1
+            assert p.col == 16 + 128 * p.table + p.f0
+            assert col is None or p.col == col  # one contiguous run of dst columns
+            col = p.col + p.dim
+            assert p.dim in (16, 32, 64, 128, 256, 512) and p.f0 % 4 == 0
+        assert len(plan.runs(r)) == 1
+    assert (seen == 1).all()
+    if world in (1, 2, 4, 8):  # 3328 features cut into equal slabs: no padding
+        assert plan.widths == [3328 // world] * world and plan.slab_ld == 3328 // world
+    assert len(plan.assembly_launches()) == 1
+    assert plan_features([5, 7], 2) == [(0, 5), (5, 12)]  # unsplittable tables
 
 
 def _worker(rank, world, port, sizes, result_q):
@@ -43,24 +59,47 @@ def _worker(rank, world, port, sizes, result_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     rng = np.random.default_rng(0)
-    dims = [16, 32, 16, 48, 16]
-    B, P, k = 40, 6, 3
+    dims = [16, 32, 16, 48, 16, 128, 96]
+    B, P, k = 41, 6, 3
     tabs = [rng.random((r, d), dtype=np.float32) for r, d in zip(sizes, dims)]
     idx = [rng.integers(1, r + 1, (B, P)) for r in sizes]
-    for spread in (False, True):
-        assignment = plan_tables(len(dims), world, sizes=sizes if spread else None)
-        layout = ShardLayout(dims, k, assignment)
-        sp = ShardedPreallocation(layout, rank, world, B, torch.float32, torch.device("cpu"))
-        mine = assignment[rank]
-        # stand-in for et_maplookup_prealloc into the slab (dst_row_off 0 + running)
-        slab = orc.maplookup_prealloc([tabs[t] for t in mine], [idx[t] for t in mine])
-        sp.slab[:, :slab.shape[1]] = torch.from_numpy(slab)
-        g = sp.exchange().numpy()
-        dst = np.zeros((B, layout.ld), np.float32)
-        for shift, rows, offs in sp.assembly_launches():
-            _concat_numpy(g, layout.slab_ld, shift, rows, offs, dst)
-        ref = orc.maplookup_prealloc(tabs, idx, prependrows=k)
-        result_q.put((rank, spread, bool(np.array_equal(dst[:, k:], ref[:, k:]))))
+    ref = orc.maplookup_prealloc(tabs, idx, prependrows=k)
+
+    class OracleShard(ShardedMapLookup):
+        """Device kernels replaced by the oracle / numpy (same semantics)."""
+
+        def lookup_chunk(self, piece_tables, piece_idx, b0, b1):
+            if piece_tables:
+                s = orc.maplookup_prealloc(piece_tables, [i[b0:b1] for i in piece_idx])
+                self.slab[b0:b1, :s.shape[1]] = torch.from_numpy(s)
+
+        def assemble_chunk(self, gathered, dst):
+            g = gathered.numpy()
+            for shift, rows, offs in self.launches:
+                for r, (n, o) in enumerate(zip(rows, offs)):
+                    if n:
+                        dst[:, o:o + n] = torch.from_numpy(g[r][:, shift:shift + n])
+
+    plans = {"table": ShardPlan.tablewise(dims, world, k),
+             "table_spread": ShardPlan.tablewise(dims, world, k, sizes=sizes),
+             "feature": ShardPlan.featurewise(dims, world, k, granule=16)}
+    for name, plan in plans.items():
+        ps = plan.pieces[rank]
+        ptabs = [np.ascontiguousarray(tabs[p.table][:, p.f0:p.f0 + p.dim]) for p in ps]
+        pidx = [idx[p.table] for p in ps]
+        for exchange, chunks in (("allgather", 1), ("allgather", 3), ("alltoall", 1)):
+            sm = OracleShard(plan, rank, world, B, torch.float32, torch.device("cpu"),
+                             exchange=exchange, chunks=chunks)
+            if exchange == "allgather":
+                dst = torch.zeros((B, plan.ld))
+                sm(ptabs, pidx, dst)
+                ok = np.array_equal(dst.numpy()[:, k:], ref[:, k:])
+            else:
+                dst = torch.zeros((sm.mine, plan.ld))
+                sm(ptabs, pidx, dst)
+                lo, hi = sm.split[rank], sm.split[rank + 1]
+                ok = np.array_equal(dst.numpy()[:, k:], ref[lo:hi, k:])
+            result_q.put((rank, name, exchange, chunks, bool(ok)))
     dist.destroy_process_group()
 
 
@@ -70,16 +109,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_sharded_prealloc_world2():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_prealloc_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    sizes = [50, 400, 30, 70, 1000]
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, sizes, q)) for r in range(2)]
+    sizes = [50, 400, 30, 70, 1000, 20, 333]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
         assert p.exitcode == 0
-    res = [q.get(timeout=5) for _ in range(4)]
-    assert len(res) == 4 and all(ok for _, _, ok in res), res
+    n = world * 3 * 3
+    res = [q.get(timeout=5) for _ in range(n)]
+    assert len(res) == n and all(r[-1] for r in res), [r for r in res if not r[-1]]

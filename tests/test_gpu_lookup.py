@@ -223,18 +223,52 @@ def test_concat_slabs():
 
 
 def test_sharded_prealloc_single_rank(oracle):
-    """embtab.sharding end to end on one GPU (world 1): local fused lookup into the
-    slab, exchange, et_concat_slabs assembly — equals the unsharded Preallocation."""
-    from embtab.sharding import ShardLayout, ShardedPreallocation, plan_tables
+    """embtab.sharding end to end on one GPU (world 1, 4 pipelined chunks on a second
+    stream): fused lookup into the slab, exchange, et_concat_slabs assembly — equals
+    the unsharded Preallocation."""
+    from embtab.sharding import ShardedMapLookup, ShardPlan
 
     rng = np.random.default_rng(8)
     dims = [128] * 6
     rows = [300, 5000, 20, 800, 64, 1000]
     hs = [rng.random((r, d), dtype=np.float32) for r, d in zip(rows, dims)]
     hidx = [rng.integers(1, r + 1, (256, 20)) for r in rows]
-    layout = ShardLayout(dims, 4, plan_tables(6, 1))
-    sp = ShardedPreallocation(layout, 0, 1, 256, torch.float32, DEV)
-    dst = torch.zeros((256, layout.ld), dtype=torch.float32, device=DEV)
-    sp([table(h) for h in hs], [dev(i) for i in hidx], dst)
     ref = oracle.maplookup_prealloc(hs, hidx, prependrows=4)
-    assert bits_equal(host(dst)[:, 4:], ref[:, 4:])
+    for plan in (ShardPlan.tablewise(dims, 1, 4), ShardPlan.featurewise(dims, 1, 4)):
+        for chunks in (1, 4):
+            sp = ShardedMapLookup(plan, 0, 1, 256, torch.float32, DEV, chunks=chunks)
+            dst = torch.zeros((256, plan.ld), dtype=torch.float32, device=DEV)
+            sp([table(h) for h in hs], [dev(i) for i in hidx], dst)
+            torch.cuda.synchronize()
+            assert bits_equal(host(dst)[:, 4:], ref[:, 4:])
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_pieces_simulated_ranks(oracle, world):
+    """Feature-sharded plans on the real kernels: every simulated rank looks up its
+    pieces (column-slice views, widths 32/64/96/128...) into its slab; the stacked
+    slabs are assembled by et_concat_slabs — bit-identical to the unsharded lookup."""
+    from embtab.sharding import ShardedMapLookup, ShardPlan, piece_table
+
+    rng = np.random.default_rng(world)
+    dims = [128] * 5 + [64, 256, 48]
+    rows = [300, 5000, 20, 800, 64, 1000, 77, 129]
+    B, k = 200, 3
+    hs = [rng.random((r, d), dtype=np.float32) for r, d in zip(rows, dims)]
+    hidx = [rng.integers(1, r + 1, (B, 20)) for r in rows]
+    full = [table(h) for h in hs]
+    didx = [dev(i) for i in hidx]
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=k)
+    for plan in (ShardPlan.featurewise(dims, world, k),
+                 ShardPlan.tablewise(dims, world, k, sizes=rows)):
+        slabs = []
+        for r in range(world):
+            sm = ShardedMapLookup(plan, r, world, B, torch.float32, DEV)
+            ps = plan.pieces[r]
+            sm.lookup_chunk([piece_table(full[p.table], p) for p in ps],
+                            [didx[p.table] for p in ps], 0, B)
+            slabs.append(sm.slab)
+        dst = torch.zeros((B, plan.ld), dtype=torch.float32, device=DEV)
+        sm.assemble_chunk(torch.stack(slabs), dst)
+        torch.cuda.synchronize()
+        assert bits_equal(host(dst)[:, k:], ref[:, k:])
