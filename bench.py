@@ -67,6 +67,10 @@ def parse():
                    help="calibration only: tables above / below 4 MiB")
     p.add_argument("--rows", type=int, default=0,
                    help="calibration only: give every table this many rows (0 = Criteo)")
+    p.add_argument("--min-rows", type=int, default=0,
+                   help="calibration only: drop the tables with fewer rows")
+    p.add_argument("--max-rows", type=int, default=0,
+                   help="calibration only: drop the tables with more rows (0 = no limit)")
     return p.parse_args()
 
 
@@ -304,6 +308,9 @@ def main():
     if args.subset != "all":
         keep = [r for r in CRITEO_KAGGLE_ROWS if (r * DIM * 4 > (4 << 20)) == (args.subset == "heavy")]
         CRITEO_KAGGLE_ROWS[:] = keep
+    if args.min_rows or args.max_rows:
+        CRITEO_KAGGLE_ROWS[:] = [r for r in CRITEO_KAGGLE_ROWS if r >= args.min_rows and
+                                 (args.max_rows == 0 or r <= args.max_rows)]
     T = len(CRITEO_KAGGLE_ROWS)
     dims = [DIM] * T
     sharded = world > 1 or args.force_shard

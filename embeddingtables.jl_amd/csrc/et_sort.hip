@@ -8,8 +8,8 @@
 // the same order as the reference.
 //
 // Scan: reduce tiles -> scan tile sums (one workgroup) -> scan tiles with offset.
-// Sort pass (8- or 9-bit digit): per-tile digit histogram (LDS atomics) -> digit-major
-// exclusive scan -> stable scatter, where each 8192-key tile is ranked in 32 rounds of
+// Sort pass (8- or 9-bit digit): per-tile digit histogram (LDS atomics) -> segment-,
+// then digit-major exclusive scan -> stable scatter, where each 8192-key tile is ranked in 32 rounds of
 // 256 keys (striped, so rounds follow input order) and each round ranks a key among
 // equal digits of lower lanes by one wave ballot per digit bit + per-wave digit counts
 // in LDS.
@@ -139,26 +139,65 @@ inline int exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t m, uint
 inline int64_t scan_part_entries(int64_t m) { return cdiv64(m, kScanTile) + 1; }
 
 // --- radix sort -----------------------------------------------------------
+//
+// Segmented: the elements are up to kRsMaxSegs contiguous segments (the tables of an
+// update), each sorted on its own key range with its own number of passes — a
+// 3-row table needs one 9-bit pass, a 10 M-row table three — so the passes over
+// all segments cost sum_t n_t * passes_t instead of n * passes(max key).  Keys of
+// segment k are reduced to min(key - key_base[k], key_cap[k]) (table-local column,
+// the out-of-range sentinel clamped to the segment's largest value).  A segment with
+// passes_t passes takes part in the LAST passes_t of the P passes, so every segment
+// ends in the same buffer; its keys start in buffer (P - passes_t) % 2.
+
+constexpr int kRsMaxSegs = 32;
+
+struct RsPass {
+    int nseg;                            // segments taking part in this pass
+    uint32_t tile_off[kRsMaxSegs + 1];   // prefix of their tiles
+    uint32_t elem0[kRsMaxSegs];          // first element of the segment
+    uint32_t n[kRsMaxSegs];              // its elements
+    uint32_t pos_base[kRsMaxSegs];       // elem0 - elements of earlier taking-part segments
+    uint32_t key_base[kRsMaxSegs];
+    uint32_t key_cap[kRsMaxSegs];
+    uint32_t shift[kRsMaxSegs];
+};
+
+__device__ __forceinline__ int rs_segment(const RsPass& p, uint32_t b) {
+    int k = 0;
+    while (k + 1 < p.nseg && b >= p.tile_off[k + 1]) ++k;
+    return k;
+}
+
+template <int NB>
+__device__ __forceinline__ uint32_t rs_digit(uint32_t key, uint32_t base, uint32_t cap,
+                                             uint32_t shift) {
+    uint32_t l = key - base;
+    l = l < cap ? l : cap;
+    return (l >> shift) & (NB - 1);
+}
 
 template <int BITS>
 __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restrict__ keys,
-                                                        int64_t n, int shift,
-                                                        uint32_t* __restrict__ hist,
-                                                        int64_t nblk) {
+                                                        RsPass p, uint32_t* __restrict__ hist) {
     constexpr int NB = 1 << BITS;
     __shared__ uint32_t h[4][NB];
     const int wave = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < 4 * NB; i += kRsThreads) (&h[0][0])[i] = 0;
     __syncthreads();
-    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    const int k = rs_segment(p, blockIdx.x);
+    const uint32_t tl = blockIdx.x - p.tile_off[k], tiles = p.tile_off[k + 1] - p.tile_off[k];
+    const uint32_t n = p.n[k], kb = p.key_base[k], cap = p.key_cap[k], sh = p.shift[k];
+    const uint32_t* kp = keys + p.elem0[k];
+    const uint32_t base = tl * kRsTile;
 #pragma unroll 4
     for (int r = 0; r < kRsItems; ++r) {
-        const int64_t i = base + r * kRsThreads + threadIdx.x;
-        if (i < n) atomicAdd(&h[wave][(keys[i] >> shift) & (NB - 1)], 1u);
+        const uint32_t i = base + r * kRsThreads + threadIdx.x;
+        if (i < n) atomicAdd(&h[wave][rs_digit<NB>(kp[i], kb, cap, sh)], 1u);
     }
     __syncthreads();
+    uint32_t* hs = hist + (uint64_t)NB * p.tile_off[k];
     for (int d = threadIdx.x; d < NB; d += kRsThreads)
-        hist[(int64_t)d * nblk + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+        hs[(uint64_t)d * tiles + tl] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
 // Stable scatter of one tile: 32 rounds of 256 keys in input order; a key's rank among
@@ -169,25 +208,30 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restri
 template <int BITS>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
-    const uint32_t* __restrict__ hist_scanned, int64_t nblk) {
+    uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, RsPass p,
+    const uint32_t* __restrict__ hist_scanned) {
     constexpr int NB = 1 << BITS;
     __shared__ uint32_t base_of[NB];
     __shared__ uint32_t wcnt[4][NB];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int k = rs_segment(p, blockIdx.x);
+    const uint32_t tl = blockIdx.x - p.tile_off[k], tiles = p.tile_off[k + 1] - p.tile_off[k];
+    const uint32_t n = p.n[k], kb = p.key_base[k], cap = p.key_cap[k], sh = p.shift[k];
+    const uint32_t e0 = p.elem0[k], pb = p.pos_base[k];
+    const uint32_t* hs = hist_scanned + (uint64_t)NB * p.tile_off[k];
     for (int d = threadIdx.x; d < NB; d += kRsThreads) {
-        base_of[d] = hist_scanned[(int64_t)d * nblk + blockIdx.x];
+        base_of[d] = hs[(uint64_t)d * tiles + tl] + pb;
         wcnt[0][d] = wcnt[1][d] = wcnt[2][d] = wcnt[3][d] = 0;
     }
     __syncthreads();
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int64_t base = (int64_t)blockIdx.x * kRsTile;
+    const uint32_t base = tl * kRsTile;
     for (int r = 0; r < kRsItems; ++r) {
-        const int64_t i = base + r * kRsThreads + threadIdx.x;
+        const uint32_t i = base + r * kRsThreads + threadIdx.x;
         const bool valid = i < n;
-        const uint32_t key = valid ? kin[i] : 0u;
-        const uint32_t val = valid ? vin[i] : 0u;
-        const uint32_t d = (key >> shift) & (NB - 1);
+        const uint32_t key = valid ? kin[e0 + i] : 0u;
+        const uint32_t val = valid ? vin[e0 + i] : 0u;
+        const uint32_t d = rs_digit<NB>(key, kb, cap, sh);
         uint64_t same = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < BITS; ++b) {
@@ -220,52 +264,94 @@ struct SortBuffers {
     uint32_t* va;
     uint32_t* kb;
     uint32_t* vb;
-    uint32_t* hist;  // kRsMaxBuckets * nblk + 1
+    uint32_t* hist;  // kRsMaxBuckets * (tiles + segments) + 1
     uint32_t* part;  // scan partials
 };
 
-inline int64_t sort_hist_entries(int64_t n) { return (int64_t)kRsMaxBuckets * cdiv64(n, kRsTile) + 1; }
-
-template <int BITS>
-inline int radix_pass(SortBuffers& sb, const uint32_t* k0, const uint32_t* v0, uint32_t* k1,
-                      uint32_t* v1, int64_t n, int shift, int64_t nblk, hipStream_t s) {
-    hipLaunchKernelGGL(k_rs_hist<BITS>, dim3((unsigned)nblk), dim3(kRsThreads), 0, s, k0, n,
-                       shift, sb.hist, nblk);
-    ET_LAUNCH_CHECK("k_rs_hist");
-    int rc = exclusive_scan_u32(sb.hist, sb.hist, (int64_t)(1 << BITS) * nblk, sb.part, s);
-    if (rc != ET_OK) return rc;
-    hipLaunchKernelGGL(k_rs_scatter<BITS>, dim3((unsigned)nblk), dim3(kRsThreads), 0, s, k0, v0,
-                       k1, v1, n, shift, sb.hist, nblk);
-    ET_LAUNCH_CHECK("k_rs_scatter");
-    return ET_OK;
+inline int64_t sort_hist_entries(int64_t n, int nseg = 1) {
+    return (int64_t)kRsMaxBuckets * (cdiv64(n, kRsTile) + nseg) + 1;
 }
 
-// Stable sort of (ka, va) by the low `bits` key bits, in ceil(bits / 9) passes of equal
-// digit width (8 or 9 bits).  On return *sorted_k / *sorted_v point at the buffers (a or
-// b) holding the result.
-inline int radix_sort_pairs(SortBuffers& sb, int64_t n, int bits, uint32_t** sorted_k,
-                            uint32_t** sorted_v, hipStream_t s) {
+// One segment of a sort: elements [elem0, elem0 + n), keys reduced to
+// min(key - key_base, key_cap) < 2^bits.
+struct RsSegment {
+    uint32_t elem0, n, key_base, key_cap;
+    int bits;
+};
+
+inline int rs_passes(int bits) { return (bits + kRsMaxBits - 1) / kRsMaxBits; }
+
+// Passes over all segments; returns the number P of passes (the result is in buffer a
+// if P is even, b if odd; segment s must start in buffer (P - rs_passes(bits_s)) % 2).
+inline int rs_total_passes(const RsSegment* seg, int nseg) {
+    int P = 0;
+    for (int k = 0; k < nseg; ++k)
+        if (seg[k].n > 0 && rs_passes(seg[k].bits) > P) P = rs_passes(seg[k].bits);
+    return P;
+}
+
+inline int segmented_radix_sort(SortBuffers& sb, const RsSegment* seg, int nseg,
+                                uint32_t** sorted_k, uint32_t** sorted_v, hipStream_t s) {
+    if (nseg > kRsMaxSegs) return fail(ET_ERR_ARG, "too many sort segments");
+    const int P = rs_total_passes(seg, nseg);
     uint32_t *k0 = sb.ka, *v0 = sb.va, *k1 = sb.kb, *v1 = sb.vb;
-    if (n > 0 && bits > 0) {
-        const int64_t nblk = cdiv64(n, kRsTile);
-        if (nblk > 0x7fffffffll) return fail(ET_ERR_ARG, "sort too large");
-        const int passes = (bits + kRsMaxBits - 1) / kRsMaxBits;
-        const int width = (bits + passes - 1) / passes <= 8 ? 8 : 9;
-        for (int shift = 0; shift < bits; shift += width) {
-            const int rc = width == 8 ? radix_pass<8>(sb, k0, v0, k1, v1, n, shift, nblk, s)
-                                      : radix_pass<9>(sb, k0, v0, k1, v1, n, shift, nblk, s);
-            if (rc != ET_OK) return rc;
-            uint32_t* t = k0;
-            k0 = k1;
-            k1 = t;
-            t = v0;
-            v0 = v1;
-            v1 = t;
+    for (int pass = 0; pass < P; ++pass) {
+        RsPass rp;
+        rp.nseg = 0;
+        rp.tile_off[0] = 0;
+        uint32_t before = 0;
+        bool wide = false;
+        for (int k = 0; k < nseg; ++k) {
+            const int pt = rs_passes(seg[k].bits);
+            if (seg[k].n == 0 || pass < P - pt) continue;
+            const int width = (seg[k].bits + pt - 1) / pt;  // <= 9
+            wide |= width > 8;
+            const int j = rp.nseg++;
+            rp.tile_off[j + 1] = rp.tile_off[j] + (uint32_t)cdiv64(seg[k].n, kRsTile);
+            rp.elem0[j] = seg[k].elem0;
+            rp.n[j] = seg[k].n;
+            rp.pos_base[j] = seg[k].elem0 - before;
+            rp.key_base[j] = seg[k].key_base;
+            rp.key_cap[j] = seg[k].key_cap;
+            rp.shift[j] = (uint32_t)((pass - (P - pt)) * width);
+            before += seg[k].n;
         }
+        const uint32_t tiles = rp.tile_off[rp.nseg];
+        const int nb = wide ? 512 : 256;
+        if (wide) {
+            hipLaunchKernelGGL(k_rs_hist<9>, dim3(tiles), dim3(kRsThreads), 0, s, k0, rp, sb.hist);
+        } else {
+            hipLaunchKernelGGL(k_rs_hist<8>, dim3(tiles), dim3(kRsThreads), 0, s, k0, rp, sb.hist);
+        }
+        ET_LAUNCH_CHECK("k_rs_hist");
+        int rc = exclusive_scan_u32(sb.hist, sb.hist, (int64_t)nb * tiles, sb.part, s);
+        if (rc != ET_OK) return rc;
+        if (wide) {
+            hipLaunchKernelGGL(k_rs_scatter<9>, dim3(tiles), dim3(kRsThreads), 0, s, k0, v0, k1,
+                               v1, rp, sb.hist);
+        } else {
+            hipLaunchKernelGGL(k_rs_scatter<8>, dim3(tiles), dim3(kRsThreads), 0, s, k0, v0, k1,
+                               v1, rp, sb.hist);
+        }
+        ET_LAUNCH_CHECK("k_rs_scatter");
+        uint32_t* t = k0;
+        k0 = k1;
+        k1 = t;
+        t = v0;
+        v0 = v1;
+        v1 = t;
     }
     *sorted_k = k0;
     *sorted_v = v0;
     return ET_OK;
+}
+
+// Stable sort of n (ka, va) pairs by the low `bits` key bits (one segment).
+inline int radix_sort_pairs(SortBuffers& sb, int64_t n, int bits, uint32_t** sorted_k,
+                            uint32_t** sorted_v, hipStream_t s) {
+    if (n >= 0xffffffffll) return fail(ET_ERR_ARG, "sort too large");
+    RsSegment seg{0u, (uint32_t)n, 0u, 0xffffffffu, bits};
+    return segmented_radix_sort(sb, &seg, 1, sorted_k, sorted_v, s);
 }
 
 inline int bits_for(uint64_t maxval) {

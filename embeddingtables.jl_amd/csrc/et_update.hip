@@ -55,13 +55,19 @@ __device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, ui
 // of consecutive occurrences.
 struct KeyGrid {
     uint32_t blk_off[ET_MAX_TABLES_PER_LAUNCH + 1];
+    uint32_t in_b;  // bit t: table t's pairs go to the second sort buffer (see et_sort.hip)
 };
 
 __global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg, int ntables,
-                                                    uint32_t* __restrict__ keys,
-                                                    uint32_t* __restrict__ vals, uint32_t sent) {
+                                                    uint32_t* __restrict__ ka,
+                                                    uint32_t* __restrict__ va,
+                                                    uint32_t* __restrict__ kb,
+                                                    uint32_t* __restrict__ vb, uint32_t sent) {
     int t = 0;
     while (t + 1 < ntables && blockIdx.x >= kg.blk_off[t + 1]) ++t;
+    const bool second = (kg.in_b >> t) & 1u;
+    uint32_t* __restrict__ keys = second ? kb : ka;
+    uint32_t* __restrict__ vals = second ? vb : va;
     const et_update_desc& d = pack.d[t];
     const uint32_t pool = (uint32_t)d.pool;
     const uint32_t n_t = pool * (uint32_t)d.batch;
@@ -497,7 +503,7 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk)
         return p;
     };
     const int64_t n1 = n + 1;
-    const int64_t hist_m = sort_hist_entries(n);
+    const int64_t hist_m = sort_hist_entries(n, kRsMaxSegs);
     const int64_t scan_m = hist_m > n1 + 1 ? hist_m : n1 + 1;
     w.ka = (uint32_t*)take(4 * n1);
     w.va = (uint32_t*)take(4 * n1);
@@ -539,12 +545,23 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
         kg.blk_off[t + 1] = kg.blk_off[t] + (uint32_t)nb;
     }
     (void)kb_grid;
+    // One sort segment per table, sorted on its own column range (et_sort.hip).
+    RsSegment seg[ET_MAX_TABLES_PER_LAUNCH];
+    for (int t = 0; t < ntables; ++t) {
+        const uint32_t nr = (uint32_t)pack.d[t].nrows;
+        seg[t] = RsSegment{pack.occ_off[t], pack.occ_off[t + 1] - pack.occ_off[t],
+                           pack.row_off[t], nr, bits_for(nr)};
+    }
+    const int P = rs_total_passes(seg, ntables);
+    kg.in_b = 0;
+    for (int t = 0; t < ntables; ++t)
+        if ((P - rs_passes(seg[t].bits)) & 1) kg.in_b |= 1u << t;
     if (kg.blk_off[ntables] > 0)
         hipLaunchKernelGGL(k_build_keys, dim3(kg.blk_off[ntables]), dim3(256), 0, s, pack, kg,
-                           ntables, w.ka, w.va, sent);
+                           ntables, w.ka, w.va, w.kb, w.vb, sent);
     ET_LAUNCH_CHECK("k_build_keys");
     SortBuffers sb{w.ka, w.va, w.kb, w.vb, w.hist, w.part};
-    int rc = radix_sort_pairs(sb, n, bits_for(sent), &out.keys, &out.vals, s);
+    int rc = segmented_radix_sort(sb, seg, ntables, &out.keys, &out.vals, s);
     if (rc != ET_OK) return rc;
     hipLaunchKernelGGL(k_seg_flags, dim3((unsigned)blocks), dim3(256), 0, s, out.keys, n, w.flag);
     ET_LAUNCH_CHECK("k_seg_flags");

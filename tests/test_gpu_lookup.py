@@ -188,6 +188,43 @@ def test_criteo_shaped_sample(oracle):
     assert bits_equal(got, oracle.maplookup_prealloc(hs, hidx, nthreads=8))
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float16, np.float64, np.int32])
+def test_tiny_tables_in_striped_launch(oracle, dtype):
+    """Tiny (L1-resident) tables beside larger ones in one striped multi-table launch:
+    tables around 16 KiB, a strided (ld > D) tiny table, out-of-range indices counted
+    and contributing zero — all bit-identical to the oracle."""
+    rng = np.random.default_rng(77)
+    es = np.dtype(dtype).itemsize
+    D = 64
+    lim = (16 << 10) // (D * es)  # rows that fit the LDS stage
+    card = [3, lim, lim + 1, 1, 700, 5, 2000]
+    mk = (lambda r: rng.integers(-9, 9, (r, D)).astype(dtype)) if dtype == np.int32 else \
+        (lambda r: rng.standard_normal((r, D)).astype(dtype))
+    hs = [mk(r) for r in card]
+    B, P = 300, 20
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in card]
+    tabs = [table(h) for h in hs]
+    wide = np.zeros((5, D + 8), dtype)  # table 5 with ld = D + 8
+    wide[:, :D] = hs[5]
+    tabs[5] = et.SimpleEmbedding(dev(wide)[:, :D])
+    assert tabs[5].ld == D + 8
+    et.check_errors()
+    got = host(et.maplookup(et.PreallocationStrategy(), tabs, [dev(i) for i in hidx]))
+    assert et.check_errors() == 0
+    assert bits_equal(got, oracle.maplookup_prealloc(hs, hidx))
+    bad = [i.copy() for i in hidx]
+    bad[0][7, 3] = 4  # one past the 3-row table
+    bad[1][0, 0] = 0
+    got = host(et.maplookup(et.PreallocationStrategy(), tabs, [dev(i) for i in bad]))
+    assert et.check_errors() == 2
+    ref = oracle.maplookup_prealloc(hs, hidx)
+    # a bad index contributes a zero row (x + 0 == x): its bag equals the bag without it
+    for t, (j, k) in ((0, (7, 3)), (1, (0, 0))):
+        bag = np.delete(hidx[t][j:j + 1], k, axis=1)
+        ref[j, D * t:D * (t + 1)] = oracle.pooled_sum(hs[t], bag)[0]
+    assert bits_equal(got, ref)
+
+
 def test_fill_matches_oracle(oracle):
     from embtab import _lib
 
