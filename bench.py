@@ -61,6 +61,9 @@ def parse():
                    help="N > 1: equal feature ranges (default) or whole tables per rank")
     p.add_argument("--chunks", type=int, default=4,
                    help="N > 1: batch chunks pipelined through lookup / all-gather / concat")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="N > 1 process group: nccl (= RCCL on ROCm) or gloo (rehearsal of "
+                        "the N > 1 path with several ranks sharing one GPU)")
     p.add_argument("--no-alltoall", action="store_true",
                    help="N > 1: skip the extra all-to-all (batch-sliced output) measurement")
     p.add_argument("--subset", choices=["all", "heavy", "light"], default="all",
@@ -206,7 +209,8 @@ def bench_alltoall(plan, rank, world, B, device, tables, idx, steps, warmup):
         a2a(tables, idx, out)
     torch.cuda.synchronize()
     dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                      device=device if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     ms = 1e3 * float(el.item()) / steps
     return {"ms_per_step": ms, "value": B * len(plan.dims) * POOL / (ms * 1e-3),
@@ -299,10 +303,15 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("run N>1 under torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    local_dev = local_rank % ndev if args.backend == "gloo" else local_rank
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
     L = _lib.load()
     B = args.batch
     if args.subset != "all":
@@ -365,7 +374,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=device if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     if sharded:  # lookup-only time: the chunked lookups alone, same launches, no exchange
@@ -411,7 +421,9 @@ def main():
             "dim": DIM,
             "table_rows": CRITEO_KAGGLE_ROWS,
             "parallelism": "single GPU" if not sharded else
-                           f"{args.plan} x{world} + RCCL all-gather ({shard.chunks} chunks)",
+                           f"{args.plan} x{world} + "
+                           f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-gather "
+                           f"({shard.chunks} chunks)",
         },
         "bags_per_s": B * T * args.steps / elapsed,
         "samples_per_s": B * args.steps / elapsed,

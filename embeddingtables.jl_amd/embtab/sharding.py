@@ -266,13 +266,22 @@ class ShardedMapLookup:
                 _lib.stream_handle(dst.device)))
 
     # --- the exchange -------------------------------------------------------------------
+    def _gloo(self) -> bool:
+        import torch.distributed as dist
+
+        return dist.get_backend(self.group) == "gloo"
+
     def _all_gather(self, out: torch.Tensor, inp: torch.Tensor):
         import torch.distributed as dist
 
         if self.world == 1:
             out[0].copy_(inp)
-        elif dist.get_backend(self.group) == "gloo":  # no all_gather_into_tensor on gloo
-            dist.all_gather(list(out.unbind(0)), inp.contiguous(), group=self.group)
+        elif self._gloo():
+            # CPU rehearsal (gloo has no all_gather_into_tensor; device tensors are
+            # staged through the host so that several ranks can share one GPU)
+            host = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather(list(host.unbind(0)), inp.cpu().contiguous(), group=self.group)
+            out.copy_(host)
         else:
             dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=self.group)
 
@@ -284,9 +293,15 @@ class ShardedMapLookup:
             return
         sizes_in = [(self.split[j + 1] - self.split[j]) * self.plan.slab_ld
                     for j in range(self.world)]
-        dist.all_to_all_single(out.view(-1), inp.reshape(-1),
-                               output_split_sizes=[self.mine * self.plan.slab_ld] * self.world,
-                               input_split_sizes=sizes_in, group=self.group)
+        sizes_out = [self.mine * self.plan.slab_ld] * self.world
+        if self._gloo():
+            host = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(host.view(-1), inp.cpu().reshape(-1), sizes_out, sizes_in,
+                                   group=self.group)
+            out.copy_(host)
+        else:
+            dist.all_to_all_single(out.view(-1), inp.reshape(-1), output_split_sizes=sizes_out,
+                                   input_split_sizes=sizes_in, group=self.group)
 
     def __call__(self, piece_tables, piece_idx, dst: torch.Tensor) -> torch.Tensor:
         """Run the sharded step; ``dst`` is ``(B, k + sum D)`` (allgather) or this
