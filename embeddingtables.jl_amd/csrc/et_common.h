@@ -51,6 +51,7 @@ inline int elsize(int dtype) {
     switch (dtype) {
         case ET_F32: return 4;
         case ET_F16: return 2;
+        case ET_BF16: return 2;
         case ET_F64: return 8;
         case ET_I32: return 4;
         case ET_I64: return 8;

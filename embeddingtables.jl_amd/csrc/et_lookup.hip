@@ -653,6 +653,9 @@ int launch_group(int dtype, bool f32acc, GroupKind kind, const LookupPack& pack,
         case ET_I64:
             return launch_group_typed<int64_t, uint64_t, NT>(kind, pack, n, D, batch, dst, ld_dst,
                                                             s);
+        case ET_BF16:  // always fp32 accumulation, one RNE rounding per output element
+            return launch_group_typed<__bf16, float, NT>(kind, pack, n, D, batch, dst, ld_dst,
+                                                         s);
         case ET_F16:
             if (f32acc)
                 return launch_group_typed<_Float16, float, NT>(kind, pack, n, D, batch, dst,

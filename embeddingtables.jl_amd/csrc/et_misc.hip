@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256) void k_fill_uniform(T* __restrict__ dst, int64
         const double u = (double)(h >> 40) * (1.0 / 16777216.0);
         const double v = __fma_rn(span, u, lo);
         if constexpr (sizeof(T) == 2)
-            dst[i] = (T)(float)v;  // double -> float -> half, as the oracle does
+            dst[i] = (T)(float)v;  // double -> float -> half / bf16, as the oracle does
         else if constexpr (__is_same(T, int32_t) || __is_same(T, int64_t))
             dst[i] = (T)floor(v);
         else
@@ -88,6 +88,10 @@ extern "C" int et_fill_uniform(int dtype, void* dst, int64_t n, uint64_t seed, u
         case ET_F16:
             hipLaunchKernelGGL(et::k_fill_uniform<_Float16>, dim3(blocks), dim3(256), 0, s,
                                (_Float16*)dst, n, seed, offset, lo, span);
+            break;
+        case ET_BF16:
+            hipLaunchKernelGGL(et::k_fill_uniform<__bf16>, dim3(blocks), dim3(256), 0, s,
+                               (__bf16*)dst, n, seed, offset, lo, span);
             break;
         case ET_I32:
             hipLaunchKernelGGL(et::k_fill_uniform<int32_t>, dim3(blocks), dim3(256), 0, s,

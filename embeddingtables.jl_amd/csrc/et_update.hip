@@ -153,6 +153,31 @@ __device__ __forceinline__ float sgd_apply(float w, float acc, float eta32, doub
     return (float)__dsub_rn((double)w, __dmul_rn(eta64, (double)acc));
 }
 
+// The update of one element for any table type T with accumulator type C (the
+// typed model of include/embtab.h / oracle/embtab_oracle.c): C = T for Float64 and
+// Float16 (every Float16 op rounded to half, as Julia's), C = float for Float32,
+// BFloat16 and Float16 with ET_FLAG_F16_FP32_ACC.  eta_c = convert(T, eta) held in C.
+template <typename T, typename C, int MODE>
+__device__ __forceinline__ T sgd_apply_t(T w, C acc, C eta_c, double eta64) {
+    if constexpr (MODE == 2) {
+        const double v = __dsub_rn((double)w, __dmul_rn(eta64, (double)acc));
+        if constexpr (__is_same(T, __bf16))
+            return (T)(float)v;
+        else
+            return (T)v;
+    } else if constexpr (__is_same(C, double)) {
+        if constexpr (MODE == 0) return __fma_rn(-eta_c, acc, (double)w);
+        return __dsub_rn((double)w, __dmul_rn(eta_c, acc));
+    } else if constexpr (MODE == 0) {
+        return (T)__builtin_fmaf(-(float)eta_c, (float)acc, (float)w);
+    } else if constexpr (__is_same(C, float)) {
+        return (T)__fsub_rn((float)w, __fmul_rn(eta_c, acc));
+    } else {  // Float16 arithmetic, two roundings (-ffp-contract=off: no fma)
+        const C t = eta_c * acc;
+        return (T)(C(w) - t);
+    }
+}
+
 // Value of lane (base + g) for group g (base wave-uniform): readlane + select for <= 4
 // groups per wave, ds_bpermute otherwise.
 template <int GPW>
@@ -409,20 +434,20 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
     }
 }
 
-// Generic fallback (any dim / alignment): one wave per chunk or combined segment,
-// lanes over features, scalar loads.
-template <int MODE, bool NT>
+// Generic kernels (any dim / alignment / element type): one wave per chunk or
+// combined segment, lanes over features, scalar loads.  T is the table and gradient
+// type, C the accumulator (sgd_apply_t).
+template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const uint32_t* __restrict__ seg_start,
     const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_seg,
     const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ counters,
-    uint32_t chunk, float* __restrict__ partials, int pdim, uint32_t sent, float eta32,
-    double eta64) {
+    uint32_t chunk, C* __restrict__ partials, int pdim, uint32_t sent, C eta_c, double eta64) {
     const int lane = threadIdx.x & 63;
-    const uint32_t C = counters[kCntC];
+    const uint32_t Cn = counters[kCntC];
     const uint32_t waves = gridDim.x * 4;
-    for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < C; c += waves) {
+    for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < Cn; c += waves) {
         const uint32_t u = chunk_seg[c];
         const uint32_t pidx = c - chunk_start[u];
         const uint32_t nchunks = chunk_start[u + 1] - chunk_start[u];
@@ -434,17 +459,16 @@ __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
         if ((pack.vec_mask >> t) & 1u) continue;  // handled by the vector kernel
         const uint32_t s0 = seg0 + pidx * chunk;
         const uint32_t s1 = s0 + chunk < seg1 ? s0 + chunk : seg1;
-        const float* delta = reinterpret_cast<const float*>(d.delta);
+        const T* delta = reinterpret_cast<const T*>(d.delta);
         for (int f = lane; f < d.dim; f += 64) {
-            float acc = 0.0f;
+            C acc = C(0);
             for (uint32_t o = s0; o < s1; ++o) {
                 const uint32_t bag = (vals[o] - pack.occ_off[t]) / (uint32_t)d.pool;
-                acc = acc + delta[(uint64_t)bag * (uint64_t)d.ld_delta + f];
+                acc = acc + C(delta[(uint64_t)bag * (uint64_t)d.ld_delta + f]);
             }
             if (nchunks == 1) {
-                float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
-                                          key - pack.row_off[t]) + f;
-                store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+                T* w = col_ptr<T>(d.table, d.ld_table, d.cols_per_page, key - pack.row_off[t]) + f;
+                store_scalar<NT>(w, sgd_apply_t<T, C, MODE>(*w, acc, eta_c, eta64));
             } else {
                 partials[(uint64_t)(partial_start[u] + pidx) * pdim + f] = acc;
             }
@@ -452,12 +476,12 @@ __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
     }
 }
 
-template <int MODE, bool NT>
+template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_combine_generic(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
-    const uint32_t* __restrict__ counters, const float* __restrict__ partials, int pdim,
-    uint32_t sent, float eta32, double eta64) {
+    const uint32_t* __restrict__ counters, const C* __restrict__ partials, int pdim,
+    uint32_t sent, C eta_c, double eta64) {
     const int lane = threadIdx.x & 63;
     const uint32_t Useg = counters[kCntU];
     const uint32_t waves = gridDim.x * 4;
@@ -470,11 +494,10 @@ __global__ __launch_bounds__(256) void k_sgd_combine_generic(
         const et_update_desc& d = pack.d[t];
         if ((pack.vec_mask >> t) & 1u) continue;
         for (int f = lane; f < d.dim; f += 64) {
-            float acc = 0.0f;
+            C acc = C(0);
             for (uint32_t q = p0; q < p1; ++q) acc = acc + partials[(uint64_t)q * pdim + f];
-            float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
-                                      key - pack.row_off[t]) + f;
-            store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+            T* w = col_ptr<T>(d.table, d.ld_table, d.cols_per_page, key - pack.row_off[t]) + f;
+            store_scalar<NT>(w, sgd_apply_t<T, C, MODE>(*w, acc, eta_c, eta64));
         }
     }
 }
@@ -520,7 +543,8 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk)
     w.counters = (uint32_t*)take(4 * kCntSlots);
     w.mlist = (uint32_t*)take(4 * (n / chunk + 2));
     const int64_t max_partials = 2 * (n / chunk) + 2;
-    w.partials = (float*)take(4 * max_partials * (int64_t)(pdim > 0 ? pdim : 1));
+    // 8 bytes per partial element: float (vector path / fp32 accumulators) or double
+    w.partials = (float*)take(8 * max_partials * (int64_t)(pdim > 0 ? pdim : 1));
     w.bytes = off;
     return w;
 }
@@ -586,44 +610,84 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     return ET_OK;
 }
 
-template <int MODE, bool NT>
+template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
-                     uint32_t chunk, int pdim, uint32_t sent, float eta32, double eta64,
+                     uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
                      int vec_dim, bool any_generic, hipStream_t s) {
     static const unsigned grid = [] {
         const char* e = getenv("ET_SGD_GRID");  // experiments: workgroups of the SGD passes
         return e ? (unsigned)atoi(e) : 256u * 16u;
     }();
+    if constexpr (__is_same(T, float)) {
 #define ET_SGD_VEC(DD)                                                                         \
     case DD:                                                                                   \
         hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
                            ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg,         \
-                           w.multi, w.counters, chunk, w.partials, pdim, sent, eta32, eta64);  \
+                           w.multi, w.counters, chunk, w.partials, pdim, sent, eta_c, eta64);  \
         hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,   \
                            ntables, gr.keys, w.seg_start, w.multi, w.counters, w.mlist,        \
-                           w.partials, pdim, sent, eta32, eta64);                              \
+                           w.partials, pdim, sent, eta_c, eta64);                              \
         break;
-    switch (vec_dim) {
-        ET_SGD_VEC(16)
-        ET_SGD_VEC(32)
-        ET_SGD_VEC(64)
-        ET_SGD_VEC(128)
-        ET_SGD_VEC(256)
-        ET_SGD_VEC(512)
-        default: break;
-    }
+        switch (vec_dim) {
+            ET_SGD_VEC(16)
+            ET_SGD_VEC(32)
+            ET_SGD_VEC(64)
+            ET_SGD_VEC(128)
+            ET_SGD_VEC(256)
+            ET_SGD_VEC(512)
+            default: break;
+        }
 #undef ET_SGD_VEC
-    ET_LAUNCH_CHECK("k_sgd_chunks");
+        ET_LAUNCH_CHECK("k_sgd_chunks");
+    }
     if (any_generic) {
-        hipLaunchKernelGGL((k_sgd_chunks_generic<MODE, NT>), dim3(grid), dim3(256), 0, s, pack,
-                           ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg, w.multi,
-                           w.counters, chunk, w.partials, pdim, sent, eta32, eta64);
-        hipLaunchKernelGGL((k_sgd_combine_generic<MODE, NT>), dim3(grid), dim3(256), 0, s, pack,
-                           ntables, gr.keys, w.seg_start, w.multi, w.counters, w.partials, pdim,
-                           sent, eta32, eta64);
+        C* partials = reinterpret_cast<C*>(w.partials);
+        hipLaunchKernelGGL((k_sgd_chunks_generic<T, C, MODE, NT>), dim3(grid), dim3(256), 0, s,
+                           pack, ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg,
+                           w.multi, w.counters, chunk, partials, pdim, sent, eta_c, eta64);
+        hipLaunchKernelGGL((k_sgd_combine_generic<T, C, MODE, NT>), dim3(grid), dim3(256), 0, s,
+                           pack, ntables, gr.keys, w.seg_start, w.multi, w.counters, partials,
+                           pdim, sent, eta_c, eta64);
         ET_LAUNCH_CHECK("k_sgd_chunks_generic");
     }
     return ET_OK;
+}
+
+// convert(T, eta) for table type `dtype` (exact in the accumulator type).
+inline double convert_eta(int dtype, double eta) {
+    switch (dtype) {
+        case ET_F32: return (double)(float)eta;
+        case ET_F16: return (double)(_Float16)eta;  // correctly rounded from Float64
+        case ET_BF16: {
+            float f = (float)eta;
+            uint32_t x;
+            __builtin_memcpy(&x, &f, 4);
+            x = (x + 0x7fffu + ((x >> 16) & 1u)) & 0xffff0000u;  // RNE (eta is finite)
+            __builtin_memcpy(&f, &x, 4);
+            return (double)f;
+        }
+        default: return eta;
+    }
+}
+
+// Element type + accumulator dispatch, then MODE / NT.
+template <typename T, typename C>
+int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
+                     uint32_t chunk, int pdim, uint32_t sent, double eta_c, double eta64,
+                     int mode, bool nt, int vec_dim, bool any_generic, hipStream_t s) {
+#define ET_SGD_CALL(M, NTV)                                                                \
+    return launch_sgd_typed<T, C, M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, (C)eta_c, \
+                                          eta64, vec_dim, any_generic, s)
+    if (mode == 0) {
+        if (nt) ET_SGD_CALL(0, true);
+        ET_SGD_CALL(0, false);
+    } else if (mode == 1) {
+        if (nt) ET_SGD_CALL(1, true);
+        ET_SGD_CALL(1, false);
+    }
+    if (nt) ET_SGD_CALL(2, true);
+    ET_SGD_CALL(2, false);
+#undef ET_SGD_CALL
 }
 
 inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_out,
@@ -679,7 +743,8 @@ extern "C" int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntable
 extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
                              uint32_t flags, void* workspace, int64_t ws_bytes, void* stream) {
     et::clear_err();
-    if (dtype != ET_F32) return et::fail(ET_ERR_UNSUPPORTED, "sparse SGD supports ET_F32 only");
+    if (dtype != ET_F32 && dtype != ET_F64 && dtype != ET_F16 && dtype != ET_BF16)
+        return et::fail(ET_ERR_UNSUPPORTED, "sparse SGD: dtype %d", dtype);
     int64_t n;
     uint64_t rows;
     int pdim;
@@ -709,7 +774,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         oo += (uint32_t)(d.pool * d.batch);
         if (d.pool == 0 || d.batch == 0 || d.dim == 0) continue;
         // paged tables qualify too: their pages are 16-byte aligned by contract
-        const bool vec_ok = (d.cols_per_page > 0 || et::aligned16(d.table)) &&
+        const bool vec_ok = dtype == ET_F32 && (d.cols_per_page > 0 || et::aligned16(d.table)) &&
                             et::aligned16(d.delta) && (d.ld_table % 4 == 0) &&
                             (d.ld_delta % 4 == 0) && et::vec_dim_ok(d.dim) &&
                             (vec_dim < 0 || vec_dim == d.dim);
@@ -730,21 +795,29 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
 
     const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
     const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;
-    const float eta32 = (float)eta;
-    const double eta64 = eta;
-#define ET_SGD_CALL(M, NTV)                                                                   \
-    return et::launch_sgd_typed<M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, eta32, eta64, \
-                                        vec_dim, any_generic, s)
-    if (mode == 0) {
-        if (nt) ET_SGD_CALL(0, true);
-        ET_SGD_CALL(0, false);
-    } else if (mode == 1) {
-        if (nt) ET_SGD_CALL(1, true);
-        ET_SGD_CALL(1, false);
+    const double eta_c = et::convert_eta(dtype, eta);
+    switch (dtype) {
+        case ET_F32:
+            return et::launch_sgd_dtype<float, float>(pack, ntables, gr, w, chunk, pdim, sent,
+                                                      eta_c, eta, mode, nt, vec_dim,
+                                                      any_generic, s);
+        case ET_F64:
+            return et::launch_sgd_dtype<double, double>(pack, ntables, gr, w, chunk, pdim, sent,
+                                                         eta_c, eta, mode, nt, vec_dim,
+                                                         any_generic, s);
+        case ET_BF16:
+            return et::launch_sgd_dtype<__bf16, float>(pack, ntables, gr, w, chunk, pdim, sent,
+                                                       eta_c, eta, mode, nt, vec_dim,
+                                                       any_generic, s);
+        default:  // ET_F16
+            if (flags & ET_FLAG_F16_FP32_ACC)
+                return et::launch_sgd_dtype<_Float16, float>(pack, ntables, gr, w, chunk, pdim,
+                                                             sent, eta_c, eta, mode, nt, vec_dim,
+                                                             any_generic, s);
+            return et::launch_sgd_dtype<_Float16, _Float16>(pack, ntables, gr, w, chunk, pdim,
+                                                            sent, eta_c, eta, mode, nt, vec_dim,
+                                                            any_generic, s);
     }
-    if (nt) ET_SGD_CALL(2, true);
-    ET_SGD_CALL(2, false);
-#undef ET_SGD_CALL
 }
 
 // ---------------------------------------------------------------------------
@@ -924,12 +997,12 @@ extern "C" int et_index_build(const int64_t* idx, int32_t pool, int64_t ld_idx, 
 // ---------------------------------------------------------------------------
 namespace et {
 
-template <int MODE, bool NT>
+template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_update_indexed(
     void* __restrict__ table, int64_t ld_table, int64_t cols_per_page, int64_t nrows, int dim,
-    const float* __restrict__ delta, int64_t ld_delta, const int64_t* __restrict__ cum_col,
+    const T* __restrict__ delta, int64_t ld_delta, const int64_t* __restrict__ cum_col,
     const int64_t* __restrict__ cum_off, int64_t ubegin, int64_t uend,
-    const int64_t* __restrict__ map, float eta32, double eta64) {
+    const int64_t* __restrict__ map, C eta_c, double eta64) {
     const int lane = threadIdx.x & 63;
     const int64_t waves = (int64_t)gridDim.x * 4;
     for (int64_t e = ubegin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); e < uend; e += waves) {
@@ -939,40 +1012,28 @@ __global__ __launch_bounds__(256) void k_update_indexed(
             continue;
         }
         const int64_t k0 = cum_off[e] - 1, k1 = cum_off[e + 1] - 1;
-        float* w = col_ptr<float>(table, ld_table, cols_per_page, col);
+        T* w = col_ptr<T>(table, ld_table, cols_per_page, col);
         for (int f = lane; f < dim; f += 64) {
-            float acc = 0.0f;  // zero(Tiled) / zero!(scratchspace)
+            C acc = C(0);  // zero(Tiled) / zero!(scratchspace)
             for (int64_t k = k0; k < k1; ++k)
-                acc = acc + delta[(uint64_t)(map[k] - 1) * (uint64_t)ld_delta + f];
-            store_scalar<NT>(w + f, sgd_apply<MODE>(w[f], acc, eta32, eta64));
+                acc = acc + C(delta[(uint64_t)(map[k] - 1) * (uint64_t)ld_delta + f]);
+            store_scalar<NT>(w + f, sgd_apply_t<T, C, MODE>(w[f], acc, eta_c, eta64));
         }
     }
 }
 
-}  // namespace et
-
-extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
-                                 int64_t cols_per_page, int64_t nrows, int32_t dim, const void* delta, int64_t ld_delta,
-                                 const int64_t* cumulative_col, const int64_t* cumulative_off,
-                                 int64_t ubegin, int64_t uend, const int64_t* map, double eta,
-                                 uint32_t flags, void* stream) {
-    et::clear_err();
-    if (dtype != ET_F32) return et::fail(ET_ERR_UNSUPPORTED, "update supports ET_F32 only");
-    if (uend <= ubegin || dim == 0) return ET_OK;
-    if (ubegin < 0 || dim < 0 || ld_table < dim || ld_delta < dim || cols_per_page < 0)
-        return et::fail(ET_ERR_ARG, "bad sizes");
-    if (!table || !delta || !cumulative_col || !cumulative_off || !map)
-        return et::fail(ET_ERR_ARG, "NULL argument");
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    const int64_t nb = et::cdiv64(uend - ubegin, 4);
+template <typename T, typename C>
+int launch_update_indexed(void* table, int64_t ld_table, int64_t cols_per_page, int64_t nrows,
+                          int dim, const void* delta, int64_t ld_delta, const int64_t* cum_col,
+                          const int64_t* cum_off, int64_t ubegin, int64_t uend,
+                          const int64_t* map, double eta_c, double eta, int mode, bool nt,
+                          hipStream_t s) {
+    const int64_t nb = cdiv64(uend - ubegin, 4);
     const unsigned grid = (unsigned)(nb < 8192 ? nb : 8192);
-    const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
-    const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;
-    const float eta32 = (float)eta;
-#define ET_UI(M, NTV)                                                                             \
-    hipLaunchKernelGGL((et::k_update_indexed<M, NTV>), dim3(grid), dim3(256), 0, s, table,      \
-                       ld_table, cols_per_page, nrows, dim, (const float*)delta, ld_delta,       \
-                       cumulative_col, cumulative_off, ubegin, uend, map, eta32, eta)
+#define ET_UI(M, NTV)                                                                           \
+    hipLaunchKernelGGL((k_update_indexed<T, C, M, NTV>), dim3(grid), dim3(256), 0, s, table,   \
+                       ld_table, cols_per_page, nrows, dim, (const T*)delta, ld_delta, cum_col, \
+                       cum_off, ubegin, uend, map, (C)eta_c, eta)
     if (mode == 0) {
         if (nt) ET_UI(0, true); else ET_UI(0, false);
     } else if (mode == 1) {
@@ -983,4 +1044,39 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
 #undef ET_UI
     ET_LAUNCH_CHECK("k_update_indexed");
     return ET_OK;
+}
+
+}  // namespace et
+
+extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
+                                 int64_t cols_per_page, int64_t nrows, int32_t dim,
+                                 const void* delta, int64_t ld_delta,
+                                 const int64_t* cumulative_col, const int64_t* cumulative_off,
+                                 int64_t ubegin, int64_t uend, const int64_t* map, double eta,
+                                 uint32_t flags, void* stream) {
+    et::clear_err();
+    if (dtype != ET_F32 && dtype != ET_F64 && dtype != ET_F16 && dtype != ET_BF16)
+        return et::fail(ET_ERR_UNSUPPORTED, "update: dtype %d", dtype);
+    if (uend <= ubegin || dim == 0) return ET_OK;
+    if (ubegin < 0 || dim < 0 || ld_table < dim || ld_delta < dim || cols_per_page < 0)
+        return et::fail(ET_ERR_ARG, "bad sizes");
+    if (!table || !delta || !cumulative_col || !cumulative_off || !map)
+        return et::fail(ET_ERR_ARG, "NULL argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
+    const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;
+    const double eta_c = et::convert_eta(dtype, eta);
+#define ET_UI_T(T, C)                                                                     \
+    return et::launch_update_indexed<T, C>(table, ld_table, cols_per_page, nrows, dim, delta, \
+                                           ld_delta, cumulative_col, cumulative_off, ubegin,  \
+                                           uend, map, eta_c, eta, mode, nt, s)
+    switch (dtype) {
+        case ET_F32: ET_UI_T(float, float);
+        case ET_F64: ET_UI_T(double, double);
+        case ET_BF16: ET_UI_T(__bf16, float);
+        default:
+            if (flags & ET_FLAG_F16_FP32_ACC) ET_UI_T(_Float16, float);
+            ET_UI_T(_Float16, _Float16);
+    }
+#undef ET_UI_T
 }

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libembtab_hip.so")
 
 ET_OK = 0
-ET_F32, ET_F16, ET_F64, ET_I32, ET_I64 = 0, 1, 2, 3, 4
+ET_F32, ET_F16, ET_F64, ET_I32, ET_I64, ET_BF16 = 0, 1, 2, 3, 4, 5
 ET_FLAG_NONTEMPORAL = 1
 ET_FLAG_F16_FP32_ACC = 2
 ET_FLAG_EXACT_UPDATE = 4
@@ -29,6 +29,7 @@ TORCH_TO_ET = {
     torch.float64: ET_F64,
     torch.int32: ET_I32,
     torch.int64: ET_I64,
+    torch.bfloat16: ET_BF16,
 }
 
 # Every entry point declared in include/embtab.h.

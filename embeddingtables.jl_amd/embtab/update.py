@@ -206,8 +206,14 @@ def gettranslations(indexer: AbstractIndexer):
 
 # --- update! ------------------------------------------------------------------------------------
 
-def _sgd_flags(fused: bool, nontemporal: bool, f64_alpha: bool = False, exact: bool = False):
+_UPDATE_DTYPES = (torch.float32, torch.float64, torch.float16, torch.bfloat16)
+
+
+def _sgd_flags(fused: bool, nontemporal: bool, f64_alpha: bool = False, exact: bool = False,
+               f16_fp32_acc: bool = False):
     flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
+    if f16_fp32_acc:
+        flags |= _lib.ET_FLAG_F16_FP32_ACC
     if not fused:
         flags |= _lib.ET_FLAG_SGD_UNFUSED
         if f64_alpha:
@@ -220,8 +226,10 @@ def _sgd_flags(fused: bool, nontemporal: bool, f64_alpha: bool = False, exact: b
 def _update_desc(table: AbstractEmbeddingTable, grad: SparseEmbeddingUpdate) -> _lib.UpdateDesc:
     I = _check_idx(grad.indices)
     delta = grad.delta
-    if table.dtype != torch.float32 or delta.dtype != torch.float32:
-        raise NotImplementedError("the fused update supports Float32 tables and gradients")
+    if table.dtype not in _UPDATE_DTYPES or delta.dtype != table.dtype:
+        raise NotImplementedError(
+            f"update of a {table.dtype} table with a {delta.dtype} gradient (supported: "
+            "Float32 / Float64 / Float16 / BFloat16 tables with gradients of the same type)")
     B = int(I.shape[0])
     P = 1 if I.dim() == 1 else int(I.shape[1])
     D, R = table.size()
@@ -234,18 +242,19 @@ def _update_desc(table: AbstractEmbeddingTable, grad: SparseEmbeddingUpdate) -> 
                            I.data_ptr(), 1 if I.dim() == 1 else _ld(I), B, cpp)
 
 
-def _sparse_sgd(descs, eta: float, flags: int, device):
+def _sparse_sgd(descs, eta: float, flags: int, device, dtype=torch.float32):
     L = _lib.load()
     n = len(descs)
     arr = (_lib.UpdateDesc * n)(*descs)
     nb = ctypes.c_int64(0)
     _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), n, ctypes.byref(nb)))
     ws = _workspace(nb.value, device, "sgd")
-    _lib.check(L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(arr), n, float(eta), flags,
-                               ws.data_ptr(), ws.numel(), _lib.stream_handle(device)))
+    _lib.check(L.et_sparse_sgd(_lib.TORCH_TO_ET[dtype], ctypes.addressof(arr), n, float(eta),
+                               flags, ws.data_ptr(), ws.numel(), _lib.stream_handle(device)))
 
 
-def update_(*args, nontemporal: bool | None = None, exact: bool = False, **kw):
+def update_(*args, nontemporal: bool | None = None, exact: bool = False,
+            f16_fp32_acc: bool = False, **kw):
     """Julia's ``update!`` (multiple dispatch on the argument types):
 
     * ``update_(opt::Descent, table, grad, [indexer], [nontemporal])`` — single table,
@@ -257,36 +266,39 @@ def update_(*args, nontemporal: bool | None = None, exact: bool = False, **kw):
 
     ``exact=True`` sums every column's gradient serially (bit-identical to the
     reference even for hot columns); the default splits occurrence lists longer than
-    512 into partial sums combined in a fixed order (deterministic)."""
+    512 into partial sums combined in a fixed order (deterministic).  Float16 tables
+    use Julia's Float16 arithmetic unless ``f16_fp32_acc`` (sums in Float32)."""
     if args and isinstance(args[0], Descent):
         opt = args[0]
         if isinstance(args[1], AbstractEmbeddingTable):
             table, grad = args[1], args[2]
             nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
-            _update_single(opt, table, grad, nt, exact)
+            _update_single(opt, table, grad, nt, exact, f16_fp32_acc)
             return None
         tables, grads = list(args[1]), list(args[2])
         nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
-        _update_multi(opt, tables, grads, nt, exact, **kw)
+        _update_multi(opt, tables, grads, nt, exact, f16_fp32_acc, **kw)
         return None
     table, grad, indexer, alpha = args[:4]
     nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
-    _update_from_indexer(table, grad, indexer, float(alpha), nt)
+    _update_from_indexer(table, grad, indexer, float(alpha), nt, f16_fp32_acc)
     return None
 
 
 def _update_single(opt: Descent, table, grad: SparseEmbeddingUpdate, nontemporal: bool,
-                   exact: bool):
+                   exact: bool, f16_fp32_acc: bool = False):
     if grad.indices.numel() == 0:
         return
     d = _update_desc(table, grad)
     fused = fused_update_path(table)
-    # convert(eltype(table), opt.eta): the fp32 kernel rounds eta to Float32 itself
-    _sparse_sgd([d], opt.eta, _sgd_flags(fused, nontemporal, False, exact), table.device)
+    # convert(eltype(table), opt.eta): the library rounds eta to the table type itself
+    _sparse_sgd([d], opt.eta, _sgd_flags(fused, nontemporal, False, exact, f16_fp32_acc),
+                table.device, table.dtype)
 
 
-def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool, num_splits=4,
-                  nthreads=None, scratchspaces=None, telemetry_cb=None, indexers=None):
+def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
+                  f16_fp32_acc: bool = False, num_splits=4, nthreads=None, scratchspaces=None,
+                  telemetry_cb=None, indexers=None):
     if len(tables) != len(grads):
         raise ArgumentError("tables and grads differ in length")
     if telemetry_cb is not None:
@@ -298,18 +310,18 @@ def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool, n
     for A, g in zip(tables, grads):
         if g.indices.numel() == 0:
             continue
-        groups.setdefault(fused_update_path(A), []).append(_update_desc(A, g))
+        groups.setdefault((fused_update_path(A), A.dtype), []).append(_update_desc(A, g))
     if not groups:
         return
     dev = tables[0].device
-    for fused, descs in groups.items():
-        flags = _sgd_flags(fused, nontemporal, not fused, exact)
+    for (fused, dtype), descs in groups.items():
+        flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc)
         for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
-            _sparse_sgd(descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH], opt.eta, flags, dev)
+            _sparse_sgd(descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH], opt.eta, flags, dev, dtype)
 
 
 def _update_from_indexer(table, grad: SparseEmbeddingUpdate, indexer: AbstractIndexer,
-                         alpha: float, nontemporal: bool):
+                         alpha: float, nontemporal: bool, f16_fp32_acc: bool = False):
     base = indexer.I if isinstance(indexer, IndexerView) else indexer
     if base.cumulative is None:
         raise ArgumentError("indexer is empty: call index_(indexer, grad.indices, maxindex)")
@@ -320,16 +332,17 @@ def _update_from_indexer(table, grad: SparseEmbeddingUpdate, indexer: AbstractIn
     if e <= b:
         return
     delta = grad.delta
-    if table.dtype != torch.float32 or delta.dtype != torch.float32:
-        raise NotImplementedError("the update supports Float32 tables and gradients")
+    if table.dtype not in _UPDATE_DTYPES or delta.dtype != table.dtype:
+        raise NotImplementedError(f"update of a {table.dtype} table with a {delta.dtype} gradient")
     D, R = table.size()
     cum = base.cumulative  # (U+1, 2) view of the (2, n+1) buffer
     fused = fused_update_path(table)
     tp, cpp = table.device_table()
     _lib.check(_lib.load().et_update_indexed(
-        _lib.ET_F32, tp, table.ld, cpp, R, D, delta.data_ptr(), _ld(delta),
+        _lib.TORCH_TO_ET[table.dtype], tp, table.ld, cpp, R, D, delta.data_ptr(), _ld(delta),
         cum[:, 0].data_ptr(), cum[:, 1].data_ptr(), b, e, base.map.data_ptr(), alpha,
-        _sgd_flags(fused, nontemporal), _lib.stream_handle(table.device)))
+        _sgd_flags(fused, nontemporal, f16_fp32_acc=f16_fp32_acc),
+        _lib.stream_handle(table.device)))
 
 
 def optimise_update_(opt, x, xbar: SparseEmbeddingUpdate, indexer=None, nontemporal=True):

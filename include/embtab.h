@@ -54,13 +54,15 @@ extern "C" {
 #define ET_F64 2
 #define ET_I32 3
 #define ET_I64 4
+#define ET_BF16 5 /* bfloat16 tables: pooled sums accumulate in fp32 and round once (RNE);
+                     not a reference type (Julia's reference never uses BFloat16) */
 
 /* Flags (bitwise OR). */
 #define ET_FLAG_NONTEMPORAL 1u   /* non-temporal stores of outputs / updated rows
                                     (reference Val{Nontemporal}, src/sparseupdate.jl:165) */
-#define ET_FLAG_F16_FP32_ACC 2u  /* F16 pooled sums accumulate in fp32 and round once;
-                                    default F16 mode rounds to fp16 after every add like
-                                    Julia Float16 arithmetic */
+#define ET_FLAG_F16_FP32_ACC 2u  /* F16 pooled sums (and F16 SGD sums) accumulate in fp32
+                                    and round once; default F16 mode rounds to fp16 after
+                                    every add like Julia Float16 arithmetic */
 #define ET_FLAG_EXACT_UPDATE 4u  /* sparse SGD: never split a hot row's occurrence list, so
                                     every row's gradient is summed serially in occurrence
                                     order (bit-identical to the reference, slower on skew) */
@@ -154,7 +156,12 @@ int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntables, int64_t*
  *     acc = +0 ; for each occurrence (in occurrence order) of r, in bag j: acc += delta_t[:, j]
  *     table_t[:, r] = muladd(-eta, acc, table_t[:, r])   (default: fused, Float32(eta))
  *                   = table_t[:, r] - eta*acc            (ET_FLAG_SGD_UNFUSED)
- * Only ET_F32 tables are supported.  Without ET_FLAG_EXACT_UPDATE, occurrence lists
+ * dtype ET_F32 (the reference's tested type; vector kernels), ET_F64, ET_F16 and
+ * ET_BF16 (generic kernels): the table and delta share the element type T, eta is
+ * convert(T, eta); Float64 accumulates in double, Float16 in Julia Float16 arithmetic
+ * (every op rounded to half) or in fp32 with ET_FLAG_F16_FP32_ACC, BFloat16 in fp32;
+ * the fused muladd of 16-bit types is one fp32 fma rounded to T (oracle/embtab_oracle.c
+ * states the exact model).  Without ET_FLAG_EXACT_UPDATE, occurrence lists
  * longer than the library's chunk length are summed as per-chunk partial sums
  * combined in chunk order (deterministic, not bit-identical to the serial sum).
  * Replaces update!(::Descent, table, ::SparseEmbeddingUpdate, indexer, Val(NT)) —

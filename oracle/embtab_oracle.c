@@ -23,6 +23,7 @@ int orc_elsize(int dtype) {
         case ORC_F64: return 8;
         case ORC_I32: return 4;
         case ORC_I64: return 8;
+        case ORC_BF16: return 2;
         default: return 0;
     }
 }
@@ -88,6 +89,21 @@ float orc_f16_to_f32(uint16_t h) {
     return f;
 }
 
+uint16_t orc_f32_to_bf16(float f) {
+    uint32_t x;
+    memcpy(&x, &f, 4);
+    if ((x & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((x >> 16) | 0x40u);
+    x += 0x7fffu + ((x >> 16) & 1u);
+    return (uint16_t)(x >> 16);
+}
+
+float orc_bf16_to_f32(uint16_t h) {
+    uint32_t x = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &x, 4);
+    return f;
+}
+
 /* Julia Float16 `a + b` = Float16(Float32(a) + Float32(b)). */
 static inline uint16_t f16_add(uint16_t a, uint16_t b) {
     return orc_f32_to_f16(orc_f16_to_f32(a) + orc_f16_to_f32(b));
@@ -135,9 +151,12 @@ void orc_gather(int dtype, const void* table, int64_t ld_table, int32_t dim, con
 #define ADD_WRAP_I32(a, b) ((int32_t)((uint32_t)(a) + (uint32_t)(b)))
 #define ADD_WRAP_I64(a, b) ((int64_t)((uint64_t)(a) + (uint64_t)(b)))
 
-static void pooled_f16_fp32acc(const uint16_t* A, int64_t ld_table, int32_t dim,
-                               const int64_t* idx, int32_t pool, int64_t ld_idx, int64_t batch,
-                               uint16_t* O, int64_t ld_dst) {
+/* 16-bit tables summed in fp32 (first row converted, later rows added in pool order),
+ * one rounding per output element: fp16 with f16_fp32_acc, and bfloat16. */
+static void pooled_16_fp32acc(const uint16_t* A, int64_t ld_table, int32_t dim,
+                              const int64_t* idx, int32_t pool, int64_t ld_idx, int64_t batch,
+                              uint16_t* O, int64_t ld_dst, float (*to32)(uint16_t),
+                              uint16_t (*from32)(float)) {
     float acc[4096];
     for (int64_t j = 0; j < batch; j++) {
         uint16_t* vO = O + (size_t)j * ld_dst;
@@ -148,11 +167,11 @@ static void pooled_f16_fp32acc(const uint16_t* A, int64_t ld_table, int32_t dim,
             for (int32_t i = 0; i < pool; i++) {
                 const uint16_t* vA = A + (size_t)(I[i] - 1) * ld_table + k0;
                 if (i == 0)
-                    for (int32_t k = 0; k < kn; k++) acc[k] = orc_f16_to_f32(vA[k]);
+                    for (int32_t k = 0; k < kn; k++) acc[k] = to32(vA[k]);
                 else
-                    for (int32_t k = 0; k < kn; k++) acc[k] += orc_f16_to_f32(vA[k]);
+                    for (int32_t k = 0; k < kn; k++) acc[k] += to32(vA[k]);
             }
-            for (int32_t k = 0; k < kn; k++) vO[k0 + k] = orc_f32_to_f16(acc[k]);
+            for (int32_t k = 0; k < kn; k++) vO[k0 + k] = from32(acc[k]);
         }
     }
 }
@@ -167,10 +186,15 @@ void orc_pooled_sum(int dtype, const void* table, int64_t ld_table, int32_t dim,
         case ORC_I64: POOLED_BODY(int64_t, ADD_WRAP_I64); break;
         case ORC_F16:
             if (f16_fp32_acc)
-                pooled_f16_fp32acc((const uint16_t*)table, ld_table, dim, idx, pool, ld_idx,
-                                   batch, (uint16_t*)dst, ld_dst);
+                pooled_16_fp32acc((const uint16_t*)table, ld_table, dim, idx, pool, ld_idx,
+                                  batch, (uint16_t*)dst, ld_dst, orc_f16_to_f32,
+                                  orc_f32_to_f16);
             else
                 POOLED_BODY(uint16_t, f16_add);
+            break;
+        case ORC_BF16:
+            pooled_16_fp32acc((const uint16_t*)table, ld_table, dim, idx, pool, ld_idx, batch,
+                              (uint16_t*)dst, ld_dst, orc_bf16_to_f32, orc_f32_to_bf16);
             break;
         default: break;
     }
@@ -504,9 +528,154 @@ void orc_sgd_f32(const orc_update_desc* d, double eta, int fused, int dense_inde
     free(map);
 }
 
+/* ------------------------------------------------------------------------- */
+/* update of Float64 / Float16 / BFloat16 tables                              */
+/* ------------------------------------------------------------------------- */
+/* The same two reference kernels (src/sparseupdate.jl:57-129) evaluated in the
+ * table's element type T, with an accumulator type C: C = T for Float64 and for
+ * Float16 (Julia Float16 arithmetic: every add / mul / sub rounded to half), C =
+ * Float32 for BFloat16 and for Float16 with acc32 (ET_FLAG_F16_FP32_ACC).  alpha is
+ * convert(T, alpha0) (then held in C); the fused path is
+ * muladd(-alpha, acc, w) = T(fma32(-alpha, acc, w)) for 16-bit T (SIMD.jl's half
+ * muladd is promoted to Float32) and fma for Float64; the generic path is x - alpha*y
+ * in C, or in Float64 (alpha_f64, the multi-table path) followed by one conversion
+ * (16-bit: Float64 -> Float32 -> bf16 for BFloat16, correctly rounded for Float16).
+ * Values travel as doubles that are exact in their type. */
+
+/* Correctly rounded double -> binary16 (ties to even). */
+uint16_t orc_f64_to_f16(double v) {
+    uint64_t bits;
+    memcpy(&bits, &v, 8);
+    uint16_t sign = (uint16_t)((bits >> 48) & 0x8000u);
+    double m = fabs(v);
+    if (isnan(v)) return (uint16_t)(sign | 0x7e00u);
+    if (m >= 65520.0) return (uint16_t)(sign | 0x7c00u);
+    int e;
+    frexp(m, &e); /* m = f * 2^e, f in [0.5, 1) => floor(log2 m) = e - 1 */
+    int E = e - 1 < -14 ? -14 : e - 1;
+    double k = rint(ldexp(m, 10 - E)); /* exact scaling, RNE to an integer */
+    if (k >= 2048.0) {
+        k = 1024.0;
+        E += 1;
+    }
+    uint32_t K = (uint32_t)k;
+    if (K < 1024) return (uint16_t)(sign | K); /* subnormal (E == -14) or zero */
+    return (uint16_t)(sign | ((uint32_t)(E + 15) << 10) | (K - 1024));
+}
+
+static inline double ty_load(int dtype, const void* p, size_t i) {
+    switch (dtype) {
+        case ORC_F32: return ((const float*)p)[i];
+        case ORC_F64: return ((const double*)p)[i];
+        case ORC_F16: return orc_f16_to_f32(((const uint16_t*)p)[i]);
+        case ORC_BF16: return orc_bf16_to_f32(((const uint16_t*)p)[i]);
+    }
+    return 0.0;
+}
+
+/* double (exact in float for 16-bit types) -> T */
+static inline void ty_store_f(int dtype, void* p, size_t i, float v) {
+    switch (dtype) {
+        case ORC_F32: ((float*)p)[i] = v; break;
+        case ORC_F16: ((uint16_t*)p)[i] = orc_f32_to_f16(v); break;
+        case ORC_BF16: ((uint16_t*)p)[i] = orc_f32_to_bf16(v); break;
+    }
+}
+
+static inline void ty_store_d(int dtype, void* p, size_t i, double v) {
+    switch (dtype) {
+        case ORC_F32: ((float*)p)[i] = (float)v; break;
+        case ORC_F64: ((double*)p)[i] = v; break;
+        case ORC_F16: ((uint16_t*)p)[i] = orc_f64_to_f16(v); break;
+        case ORC_BF16: ((uint16_t*)p)[i] = orc_f32_to_bf16((float)v); break;
+    }
+}
+
+/* accumulator kind: 0 = Float64, 1 = Float32, 2 = Float16 */
+static inline int ty_acc(int dtype, int acc32) {
+    if (dtype == ORC_F64) return 0;
+    if (dtype == ORC_F16 && !acc32) return 2;
+    return 1;
+}
+
+static inline double acc_add(int ak, double a, double x) {
+    if (ak == 0) return a + x;
+    if (ak == 1) return (double)((float)a + (float)x);
+    return orc_f16_to_f32(orc_f32_to_f16((float)a + (float)x));
+}
+
+/* convert(T, alpha0) held in the accumulator type */
+double orc_convert_eta(int dtype, double eta) {
+    switch (dtype) {
+        case ORC_F32: return (float)eta;
+        case ORC_F64: return eta;
+        case ORC_F16: return orc_f16_to_f32(orc_f64_to_f16(eta));
+        case ORC_BF16: return orc_bf16_to_f32(orc_f32_to_bf16((float)eta));
+    }
+    return eta;
+}
+
+void orc_update_typed(int dtype, int acc32, void* table, int64_t ld_table, int32_t dim,
+                      const void* delta, int64_t ld_delta, const int64_t* cum_col,
+                      const int64_t* cum_off, int64_t ubegin, int64_t uend, const int64_t* map,
+                      double alpha, int fused, int alpha_f64) {
+    const int ak = ty_acc(dtype, acc32);
+    double* acc = (double*)malloc(sizeof(double) * (size_t)(dim > 0 ? dim : 1));
+    for (int64_t e = ubegin; e < uend; e++) {
+        int64_t k = cum_col[e];
+        int64_t start = cum_off[e];
+        int64_t stop = cum_off[e + 1] - 1;
+        for (int32_t f = 0; f < dim; f++) acc[f] = 0.0;
+        for (int64_t i = start; i <= stop; i++) {
+            size_t g = (size_t)(map[i - 1] - 1) * ld_delta;
+            for (int32_t f = 0; f < dim; f++)
+                acc[f] = acc_add(ak, acc[f], ty_load(dtype, delta, g + f));
+        }
+        size_t w0 = (size_t)(k - 1) * ld_table;
+        for (int32_t f = 0; f < dim; f++) {
+            double w = ty_load(dtype, table, w0 + f);
+            if (fused) {
+                if (ak == 0)
+                    ty_store_d(dtype, table, w0 + f, fma(-alpha, acc[f], w));
+                else
+                    ty_store_f(dtype, table, w0 + f,
+                               fmaf(-(float)alpha, (float)acc[f], (float)w));
+            } else if (alpha_f64) {
+                ty_store_d(dtype, table, w0 + f, w - alpha * acc[f]);
+            } else if (ak == 0) {
+                ty_store_d(dtype, table, w0 + f, w - alpha * acc[f]);
+            } else if (ak == 1) {
+                ty_store_f(dtype, table, w0 + f, (float)w - (float)alpha * (float)acc[f]);
+            } else {
+                float t = orc_f16_to_f32(orc_f32_to_f16((float)alpha * (float)acc[f]));
+                ty_store_f(dtype, table, w0 + f, (float)w - t);
+            }
+        }
+    }
+    free(acc);
+}
+
+/* orc_sgd_f32 for any table type (single table, eta converted to T). */
+void orc_sgd_typed(const orc_update_desc* d, int dtype, int acc32, double eta, int fused,
+                   int dense_indexer) {
+    int64_t n = (int64_t)d->pool * d->batch;
+    if (n <= 0) return;
+    int64_t* cum_col = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
+    int64_t* cum_off = (int64_t*)malloc(sizeof(int64_t) * (n + 1));
+    int64_t* map = (int64_t*)malloc(sizeof(int64_t) * n);
+    int64_t U = orc_index_build(d->idx, d->pool, d->ld_idx, d->batch, d->nrows, dense_indexer,
+                                cum_col, cum_off, map);
+    orc_update_typed(dtype, acc32, d->table, d->ld_table, d->dim, d->delta, d->ld_delta, cum_col,
+                     cum_off, 0, U, map, orc_convert_eta(dtype, eta), fused, 0);
+    free(cum_col);
+    free(cum_off);
+    free(map);
+}
+
 typedef struct {
     const orc_update_desc* descs;
     int32_t ntables;
+    int dtype, acc32;
     double eta;
     const int32_t* fused;
     int num_splits;
@@ -545,7 +714,13 @@ static void* multi_worker(void* arg) {
         int64_t stop = j * split + 1 < len_c ? j * split + 1 : len_c;
         int64_t ubegin = start - 1, uend = stop - 1; /* entries start..stop-1, 0-based */
         if (uend <= ubegin) continue;
-        if (c->fused[i - 1])
+        if (c->dtype != ORC_F32)
+            orc_update_typed(c->dtype, c->acc32, d->table, d->ld_table, d->dim, d->delta,
+                             d->ld_delta, c->cum_col[i - 1], c->cum_off[i - 1], ubegin, uend,
+                             c->map[i - 1],
+                             c->fused[i - 1] ? orc_convert_eta(c->dtype, c->eta) : c->eta,
+                             c->fused[i - 1], !c->fused[i - 1]);
+        else if (c->fused[i - 1])
             orc_update_specialized_f32((float*)d->table, d->ld_table, d->dim,
                                        (const float*)d->delta, d->ld_delta, c->cum_col[i - 1],
                                        c->cum_off[i - 1], ubegin, uend, c->map[i - 1],
@@ -560,10 +735,17 @@ static void* multi_worker(void* arg) {
 
 void orc_sgd_multi_f32(const orc_update_desc* descs, int32_t ntables, double eta,
                        const int32_t* fused, int num_splits, int nthreads) {
+    orc_sgd_multi_typed(descs, ntables, ORC_F32, 0, eta, fused, num_splits, nthreads);
+}
+
+void orc_sgd_multi_typed(const orc_update_desc* descs, int32_t ntables, int dtype, int acc32,
+                         double eta, const int32_t* fused, int num_splits, int nthreads) {
     if (ntables <= 0) return;
     if (nthreads <= 0) nthreads = 1;
     if (num_splits <= 0) num_splits = 4;
     multi_ctx c;
+    c.dtype = dtype;
+    c.acc32 = acc32;
     c.descs = descs;
     c.ntables = ntables;
     c.eta = eta;
@@ -632,6 +814,7 @@ static void fill_range(const fill_ctx* c, int64_t b, int64_t e) {
             case ORC_F32: ((float*)c->dst)[i] = (float)v; break;
             case ORC_F64: ((double*)c->dst)[i] = v; break;
             case ORC_F16: ((uint16_t*)c->dst)[i] = orc_f32_to_f16((float)v); break;
+            case ORC_BF16: ((uint16_t*)c->dst)[i] = orc_f32_to_bf16((float)v); break;
             case ORC_I32: ((int32_t*)c->dst)[i] = (int32_t)floor(v); break;
             case ORC_I64: ((int64_t*)c->dst)[i] = (int64_t)floor(v); break;
         }

@@ -25,6 +25,7 @@
 #define ORC_F64 2
 #define ORC_I32 3
 #define ORC_I64 4
+#define ORC_BF16 5 /* not a reference type: fp32 accumulation, one RNE rounding */
 
 /* Same memory layout as et_lookup_desc / et_update_desc in include/embtab.h. */
 typedef struct orc_lookup_desc {
@@ -56,6 +57,9 @@ int orc_elsize(int dtype);
 /* fp16 <-> fp32 (round to nearest even), the conversions Julia's Float16 uses. */
 uint16_t orc_f32_to_f16(float f);
 float orc_f16_to_f32(uint16_t h);
+/* bfloat16 <-> fp32 (round to nearest even; NaN stays a quiet NaN). */
+uint16_t orc_f32_to_bf16(float f);
+float orc_bf16_to_f32(uint16_t h);
 
 /* src/lookup.jl:51-87: non-reducing lookup (bit copy). */
 void orc_gather(int dtype, const void* table, int64_t ld_table, int32_t dim, const int64_t* idx,
@@ -112,6 +116,19 @@ void orc_sgd_f32(const orc_update_desc* d, double eta, int fused, int dense_inde
  * generic path sees eta as Float64. */
 void orc_sgd_multi_f32(const orc_update_desc* descs, int32_t ntables, double eta,
                        const int32_t* fused, int num_splits, int nthreads);
+
+/* Float64 / Float16 / BFloat16 tables (acc32: Float16 summed in Float32), see
+ * embtab_oracle.c "update of Float64 / Float16 / BFloat16 tables" for the arithmetic. */
+uint16_t orc_f64_to_f16(double v);
+double orc_convert_eta(int dtype, double eta);
+void orc_update_typed(int dtype, int acc32, void* table, int64_t ld_table, int32_t dim,
+                      const void* delta, int64_t ld_delta, const int64_t* cum_col,
+                      const int64_t* cum_off, int64_t ubegin, int64_t uend, const int64_t* map,
+                      double alpha, int fused, int alpha_f64);
+void orc_sgd_typed(const orc_update_desc* d, int dtype, int acc32, double eta, int fused,
+                   int dense_indexer);
+void orc_sgd_multi_typed(const orc_update_desc* descs, int32_t ntables, int dtype, int acc32,
+                         double eta, const int32_t* fused, int num_splits, int nthreads);
 
 /* Counter-based synthetic data, identical bits to et_fill_uniform /
  * et_fill_index_uniform of the HIP library. */

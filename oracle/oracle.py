@@ -21,7 +21,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liborc.so")
 
-F32, F16, F64, I32, I64 = 0, 1, 2, 3, 4
+F32, F16, F64, I32, I64, BF16 = 0, 1, 2, 3, 4, 5
 _DTYPES = {
     np.dtype(np.float32): F32,
     np.dtype(np.float16): F16,
@@ -88,6 +88,12 @@ def lib():
         L.orc_index_build.restype = i64
         L.orc_sgd_f32.argtypes = [vp, dbl, ctypes.c_int, ctypes.c_int]
         L.orc_sgd_multi_f32.argtypes = [vp, i32, dbl, vp, ctypes.c_int, ctypes.c_int]
+        L.orc_sgd_typed.argtypes = [vp, ctypes.c_int, ctypes.c_int, dbl, ctypes.c_int,
+                                    ctypes.c_int]
+        L.orc_sgd_multi_typed.argtypes = [vp, i32, ctypes.c_int, ctypes.c_int, dbl, vp,
+                                          ctypes.c_int, ctypes.c_int]
+        L.orc_f64_to_f16.argtypes = [dbl]
+        L.orc_f64_to_f16.restype = ctypes.c_uint16
         L.orc_fill_uniform.argtypes = [ctypes.c_int, vp, i64, u64, u64, dbl, dbl, ctypes.c_int]
         L.orc_fill_index_uniform.argtypes = [vp, i64, i64, u64, u64, ctypes.c_int]
         L.orc_f32_to_f16.argtypes = [ctypes.c_float]
@@ -101,8 +107,24 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
-def _dt(a: np.ndarray) -> int:
+def _dt(a: np.ndarray, bf16: bool = False) -> int:
+    """Element type code; bfloat16 arrays are uint16 bit patterns flagged by ``bf16``."""
+    if bf16:
+        assert a.dtype == np.uint16
+        return BF16
     return _DTYPES[a.dtype]
+
+
+def f32_to_bf16(x: np.ndarray) -> np.ndarray:
+    """float32 -> bfloat16 bits (uint16), round to nearest even (NaN -> quiet NaN)."""
+    b = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    nan = (b & 0x7fffffff) > 0x7f800000
+    r = ((b + 0x7fff + ((b >> 16) & 1)) >> 16).astype(np.uint16)
+    return np.where(nan, ((b >> 16) | 0x40).astype(np.uint16), r)
+
+
+def bf16_to_f32(h: np.ndarray) -> np.ndarray:
+    return (np.ascontiguousarray(h, np.uint16).astype(np.uint32) << 16).view(np.float32)
 
 
 def _idx2d(I: np.ndarray) -> np.ndarray:
@@ -113,35 +135,36 @@ def _idx2d(I: np.ndarray) -> np.ndarray:
 
 # --- lookup ---------------------------------------------------------------------
 
-def gather(table: np.ndarray, I: np.ndarray) -> np.ndarray:
+def gather(table: np.ndarray, I: np.ndarray, bf16: bool = False) -> np.ndarray:
     """src/lookup.jl:51-87 — out[j] = table[I[j]-1] (bit copy)."""
     table = np.ascontiguousarray(table)
     I = np.ascontiguousarray(I, dtype=np.int64)
     out = np.empty((I.shape[0], table.shape[1]), dtype=table.dtype)
-    lib().orc_gather(_dt(table), _ptr(table), table.shape[1], table.shape[1], _ptr(I),
+    lib().orc_gather(_dt(table, bf16), _ptr(table), table.shape[1], table.shape[1], _ptr(I),
                      I.shape[0], _ptr(out), out.shape[1])
     return out
 
 
-def pooled_sum(table: np.ndarray, I: np.ndarray, f16_fp32_acc: bool = False) -> np.ndarray:
+def pooled_sum(table: np.ndarray, I: np.ndarray, f16_fp32_acc: bool = False,
+               bf16: bool = False) -> np.ndarray:
     """src/lookup.jl:108-165 — out[j] = sum_i table[I[j, i]-1], sequential in i."""
     table = np.ascontiguousarray(table)
     I = _idx2d(I)
     B, P = I.shape
     out = np.empty((B, table.shape[1]), dtype=table.dtype)
-    lib().orc_pooled_sum(_dt(table), _ptr(table), table.shape[1], table.shape[1], _ptr(I), P, P,
+    lib().orc_pooled_sum(_dt(table, bf16), _ptr(table), table.shape[1], table.shape[1], _ptr(I), P, P,
                          B, _ptr(out), out.shape[1], int(f16_fp32_acc))
     return out
 
 
-def lookup(table: np.ndarray, I: np.ndarray) -> np.ndarray:
+def lookup(table: np.ndarray, I: np.ndarray, bf16: bool = False) -> np.ndarray:
     """Dispatch like src/lookup.jl:35-40: vector -> gather, matrix -> pooled sum."""
-    return gather(table, I) if np.ndim(I) == 1 else pooled_sum(table, I)
+    return gather(table, I, bf16) if np.ndim(I) == 1 else pooled_sum(table, I, bf16=bf16)
 
 
 def maplookup_prealloc(tables, indices, prependrows: int = 0, nthreads: int = 1,
                        worksize_div: int = 8, out: np.ndarray | None = None,
-                       f16_fp32_acc: bool = False) -> np.ndarray:
+                       f16_fp32_acc: bool = False, bf16: bool = False) -> np.ndarray:
     """src/lookup.jl:305-371 — fused concat, (B, prependrows + sum D) output."""
     tables = [np.ascontiguousarray(t) for t in tables]
     idx = [_idx2d(I) for I in indices]
@@ -155,7 +178,7 @@ def maplookup_prealloc(tables, indices, prependrows: int = 0, nthreads: int = 1,
         descs[k] = LookupDesc(_ptr(t), t.shape[1], t.shape[0], t.shape[1], I.shape[1], _ptr(I),
                               I.shape[1], off)
         off += t.shape[1]
-    lib().orc_maplookup_prealloc(_dt(out), ctypes.addressof(descs), len(tables), B, _ptr(out),
+    lib().orc_maplookup_prealloc(_dt(out, bf16), ctypes.addressof(descs), len(tables), B, _ptr(out),
                                  ld, nthreads, worksize_div, int(f16_fp32_acc))
     return out
 
@@ -190,54 +213,76 @@ def index_build(A: np.ndarray, maxindex: int, dense: bool = False):
 
 # --- update ---------------------------------------------------------------------
 
+def _upd_type(table: np.ndarray, bf16: bool) -> int:
+    code = _dt(table, bf16)
+    assert code in (F32, F64, F16, BF16) and table.flags.c_contiguous
+    return code
+
+
 def sgd(table: np.ndarray, delta: np.ndarray, I: np.ndarray, eta: float, fused: bool = True,
-        dense_indexer: bool = False) -> None:
-    """src/sparseupdate.jl:160-178 — in-place Descent update of a float32 table."""
-    assert table.dtype == np.float32 and table.flags.c_contiguous
+        dense_indexer: bool = False, bf16: bool = False, f16_fp32_acc: bool = False) -> None:
+    """src/sparseupdate.jl:160-178 — in-place Descent update; Float32 tables follow the
+    reference exactly, Float64 / Float16 / BFloat16 the typed model of
+    embtab_oracle.c (``bf16``: uint16 bit patterns; ``delta`` of the table's type)."""
+    code = _upd_type(table, bf16)
     I = _idx2d(I)
-    delta = np.ascontiguousarray(delta, np.float32)
+    delta = np.ascontiguousarray(delta, table.dtype)
     B, P = I.shape
     d = UpdateDesc(_ptr(table), table.shape[1], table.shape[0], table.shape[1], P, _ptr(delta),
                    delta.shape[1], _ptr(I), P, B)
-    lib().orc_sgd_f32(ctypes.byref(d), float(eta), int(fused), int(dense_indexer))
+    if code == F32:
+        lib().orc_sgd_f32(ctypes.byref(d), float(eta), int(fused), int(dense_indexer))
+    else:
+        lib().orc_sgd_typed(ctypes.byref(d), code, int(f16_fp32_acc), float(eta), int(fused),
+                            int(dense_indexer))
 
 
 def sgd_multi(tables, deltas, indices, eta: float, fused, num_splits: int = 4,
-              nthreads: int = 1, delta_ld: int | None = None, delta_offsets=None) -> None:
+              nthreads: int = 1, delta_ld: int | None = None, delta_offsets=None,
+              bf16: bool = False, f16_fp32_acc: bool = False) -> None:
     """src/sparseupdate.jl:199-238 — multi-table threaded update (in place).
 
     ``deltas`` is either a list of (B, D_t) arrays, or one (B, ld) array with
     ``delta_offsets[t]`` giving each table's first column (Preallocation layout).
+    Every table has the same element type.
     """
     n = len(tables)
     keep = []
     descs = (UpdateDesc * n)()
+    code = _upd_type(tables[0], bf16)
     for t in range(n):
         I = _idx2d(indices[t])
         keep.append(I)
         B, P = I.shape
         tab = tables[t]
-        assert tab.dtype == np.float32 and tab.flags.c_contiguous
+        assert _upd_type(tab, bf16) == code
+        es = tab.dtype.itemsize
         if delta_offsets is None:
-            dl = np.ascontiguousarray(deltas[t], np.float32)
+            dl = np.ascontiguousarray(deltas[t], tab.dtype)
             keep.append(dl)
             dptr, ldd = _ptr(dl), dl.shape[1]
         else:
             big = deltas
-            dptr, ldd = _ptr(big) + 4 * int(delta_offsets[t]), big.shape[1]
+            dptr, ldd = _ptr(big) + es * int(delta_offsets[t]), big.shape[1]
         descs[t] = UpdateDesc(_ptr(tab), tab.shape[1], tab.shape[0], tab.shape[1], P, dptr, ldd,
                               _ptr(I), P, B)
     fz = np.asarray([int(f) for f in fused], np.int32)
-    lib().orc_sgd_multi_f32(ctypes.addressof(descs), n, float(eta), _ptr(fz), num_splits,
-                            nthreads)
+    if code == F32:
+        lib().orc_sgd_multi_f32(ctypes.addressof(descs), n, float(eta), _ptr(fz), num_splits,
+                                nthreads)
+    else:
+        lib().orc_sgd_multi_typed(ctypes.addressof(descs), n, code, int(f16_fp32_acc),
+                                  float(eta), _ptr(fz), num_splits, nthreads)
 
 
 # --- synthetic data ---------------------------------------------------------------
 
 def fill_uniform(shape, dtype, seed: int, offset: int = 0, lo: float = 0.0, hi: float = 1.0,
                  nthreads: int = 8) -> np.ndarray:
-    a = np.empty(shape, dtype=dtype)
-    lib().orc_fill_uniform(_DTYPES[np.dtype(dtype)], _ptr(a), a.size, seed, offset, lo, hi,
+    """``dtype`` "bf16" gives bfloat16 bit patterns (uint16)."""
+    bf16 = dtype == "bf16"
+    a = np.empty(shape, dtype=np.uint16 if bf16 else dtype)
+    lib().orc_fill_uniform(BF16 if bf16 else _DTYPES[np.dtype(dtype)], _ptr(a), a.size, seed, offset, lo, hi,
                            nthreads)
     return a
 

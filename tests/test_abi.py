@@ -82,7 +82,7 @@ def test_argument_errors_need_no_gpu():
     # empty work is a no-op success
     assert L.et_gather(_lib.ET_F32, None, 16, 10, 16, None, 0, None, 16, 0, None) == 0
     # update supports F32 only
-    assert L.et_sparse_sgd(_lib.ET_F16, None, 0, 0.1, 0, None, 0, None) == -4
+    assert L.et_sparse_sgd(_lib.ET_I32, None, 0, 0.1, 0, None, 0, None) == -4
     # workspace sizing is host-only arithmetic
     d = (_lib.UpdateDesc * 1)()
     d[0] = _lib.UpdateDesc(1 << 20, 128, 1000, 128, 20, 1 << 20, 128, 1 << 20, 20, 4096)

@@ -83,6 +83,37 @@ def test_lookup_dtypes(oracle, dtype, dim):
     assert bits_equal(host(et.lookup(A, dev(v))), oracle.gather(h, v))
 
 
+@pytest.mark.parametrize("dim", [16, 128, 512, 40])
+def test_bf16_tables(oracle, dim):
+    """bfloat16 tables (fp32 accumulation, one rounding): pooled sums, gathers, the
+    fused Preallocation launch and the fill are bit-identical to the oracle."""
+    rng = np.random.default_rng(dim)
+    h = oracle.f32_to_bf16(rng.standard_normal((600, dim)).astype(np.float32))
+    A = et.SimpleEmbedding(dev(h).view(torch.bfloat16))
+    assert A.dtype == torch.bfloat16
+    I = rng.integers(1, 601, (300, 20))
+    got = et.lookup(A, dev(I))
+    assert got.dtype == torch.bfloat16
+    assert bits_equal(host(got.view(torch.int16)).view(np.uint16),
+                      oracle.pooled_sum(h, I, bf16=True))
+    v = rng.integers(1, 601, 333)
+    assert bits_equal(host(et.lookup(A, dev(v)).view(torch.int16)).view(np.uint16),
+                      oracle.gather(h, v, bf16=True))
+    hs = [h, oracle.f32_to_bf16(rng.random((50, dim), dtype=np.float32))]
+    idx = [I, rng.integers(1, 51, (300, 7))]
+    tabs = [A, et.SimpleEmbedding(dev(hs[1]).view(torch.bfloat16))]
+    out = et.maplookup(et.PreallocationStrategy(2), tabs, [dev(i) for i in idx])
+    ref = oracle.maplookup_prealloc(hs, idx, prependrows=2, bf16=True)
+    assert bits_equal(host(out.view(torch.int16)).view(np.uint16)[:, 2:], ref[:, 2:])
+    from embtab import _lib
+
+    buf = torch.empty(5000, dtype=torch.bfloat16, device=DEV)
+    _lib.check(_lib.load().et_fill_uniform(_lib.ET_BF16, buf.data_ptr(), 5000, 9, 3, -2.0, 2.0,
+                                           _lib.stream_handle()))
+    assert bits_equal(host(buf.view(torch.int16)).view(np.uint16),
+                      oracle.fill_uniform((5000,), "bf16", 9, 3, -2.0, 2.0))
+
+
 @pytest.mark.parametrize("dim", [16, 128, 24])
 def test_f16_fp32_accumulate_mode(oracle, dim):
     from embtab import _lib

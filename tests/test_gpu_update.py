@@ -211,3 +211,100 @@ def test_update_oob_skipped():
     assert et.check_errors() == 1
     out = host(A.data)
     assert (out[0] == -1).all() and (out[1] == -1).all() and not out[2:].any()
+
+
+# --- Float64 / Float16 / BFloat16 tables ---------------------------------------------------
+# No reference test covers them (parity unpinned by the reference); the oracle's typed
+# model (oracle/embtab_oracle.c, "update of Float64 / Float16 / BFloat16 tables") is
+# the definition, and the HIP path must match it bit for bit.
+
+def _typed(rng, shape, kind):
+    x = rng.standard_normal(shape).astype(np.float32)
+    if kind == "bf16":
+        from oracle import f32_to_bf16
+        return f32_to_bf16(x)
+    return x.astype({"f64": np.float64, "f16": np.float16, "f16acc": np.float16}[kind])
+
+
+def _dev_typed(a, kind):
+    t = dev(a)
+    return t.view(torch.bfloat16) if kind == "bf16" else t
+
+
+def _host_bits(t):
+    return host(t.view(torch.int16)) if t.dtype in (torch.float16, torch.bfloat16) else host(t)
+
+
+@pytest.mark.parametrize("kind", ["f64", "f16", "f16acc", "bf16"])
+@pytest.mark.parametrize("dim,static", [(64, True), (128, True), (40, False)])
+@pytest.mark.parametrize("exact", [True, False])
+def test_update_typed_vs_oracle(oracle, kind, dim, static, exact):
+    rng = np.random.default_rng(dim + len(kind))
+    ncols, B, P = 300, 256, 8
+    base = _typed(rng, (ncols, dim), kind)
+    delta = _typed(rng, (B, dim), kind)
+    I = rng.integers(1, ncols + 1, (B, P))
+    I[:, 0] = 7  # one column with 256 occurrences, another with > 512 (partials)
+    I[:, 1:4] = 11
+    A = et.SimpleEmbedding(_dev_typed(base, kind), et.Static(dim) if static else et.Dynamic)
+    from embtab.tables import fused_update_path
+
+    g = et.SparseEmbeddingUpdate(A.lookup_type, _dev_typed(delta, kind), dev(I))
+    et.update_(et.Descent(0.1), A, g, exact=exact, f16_fp32_acc=kind == "f16acc")
+    ref = base.copy()
+    oracle.sgd(ref, delta, I, 0.1, fused=fused_update_path(A), bf16=kind == "bf16",
+               f16_fp32_acc=kind == "f16acc")
+    got = _host_bits(A.data)
+    hot = np.zeros(ncols, bool)
+    hot[10] = True  # column 11: 768 occurrences, summed as ordered partials unless exact
+    if exact:
+        assert bits_equal(got, ref.view(got.dtype))
+    else:
+        assert bits_equal(got[~hot], ref.view(got.dtype)[~hot])
+        w = got[hot].view(ref.dtype)
+        r = ref[hot]
+        if kind == "bf16":
+            from oracle import bf16_to_f32
+            w, r = bf16_to_f32(w), bf16_to_f32(r)
+        tol = {"f64": 1e-12, "f16": 0.5, "f16acc": 5e-3, "bf16": 3e-2}[kind]
+        assert np.allclose(np.asarray(w, np.float64), np.asarray(r, np.float64), rtol=tol,
+                           atol=tol)
+
+
+@pytest.mark.parametrize("kind", ["f64", "f16", "bf16"])
+def test_multi_table_typed_and_indexer_view(oracle, kind):
+    """Multi-table update! of typed tables (the generic path sees Float64 eta) and the
+    IndexerView update of a typed table."""
+    rng = np.random.default_rng(3)
+    B, P, k = 200, 10, 4
+    dims, rows = (32, 128, 64), (100, 400, 50)
+    hs = [_typed(rng, (r, d), kind) for r, d in zip(rows, dims)]
+    tabs = [et.SimpleEmbedding(_dev_typed(h, kind), et.Static(d) if t != 2 else et.Dynamic)
+            for t, (h, d) in enumerate(zip(hs, dims))]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    ld = k + sum(dims)
+    big = _typed(rng, (B, ld), kind)
+    offs = np.cumsum([k] + list(dims[:-1]))
+    gbig = _dev_typed(big, kind)
+    grads = [et.SparseEmbeddingUpdate(A.lookup_type, gbig[:, o:o + d], dev(i))
+             for A, o, d, i in zip(tabs, offs, dims, hidx)]
+    et.update_(et.Descent(0.25), tabs, grads, [et.Indexer() for _ in tabs])
+    from embtab.tables import fused_update_path
+
+    refs = [h.copy() for h in hs]
+    oracle.sgd_multi(refs, big, hidx, 0.25, [fused_update_path(t) for t in tabs],
+                     delta_offsets=offs, bf16=kind == "bf16")
+    for t in range(3):
+        assert bits_equal(_host_bits(tabs[t].data), refs[t].view(_host_bits(tabs[t].data).dtype))
+    # IndexerView splits of a typed table == the single-table oracle update with alpha
+    base = _typed(rng, (100, 48), kind)
+    delta = _typed(rng, (300, 48), kind)
+    I = rng.integers(1, 101, 300)
+    A = et.SimpleEmbedding(_dev_typed(base, kind), et.Static(48))
+    g = et.SparseEmbeddingUpdate(A.lookup_type, _dev_typed(delta, kind), dev(I))
+    ix = et.index_(et.Indexer(), g.indices, 100)
+    for s in range(1, 5):
+        et.update_(A, g, et.IndexerView(ix, 4, s), 0.5)
+    ref = base.copy()
+    oracle.sgd(ref, delta, I, 0.5, fused=fused_update_path(A), bf16=kind == "bf16")
+    assert bits_equal(_host_bits(A.data), ref.view(_host_bits(A.data).dtype))

@@ -132,6 +132,24 @@ def test_f16_per_add_rounding(oracle):
     assert np.array_equal(acc.view(np.uint16), s.astype(np.float16).view(np.uint16))
 
 
+def test_bf16_fp32_accumulation(oracle):
+    """bfloat16 (not a reference type): fp32 sum in pool order, one RNE rounding."""
+    x = np.array([1.0, 1.00390625, 1.005859375, -3.14159, np.inf, 3.3895e38], np.float32)
+    assert oracle.f32_to_bf16(x).tolist() == [16256, 16256, 16257, 49225, 32640, 32639]
+    rng = np.random.default_rng(4)
+    A = oracle.f32_to_bf16(rng.standard_normal((100, 24)).astype(np.float32))
+    I = rng.integers(1, 101, (32, 20))
+    f = oracle.bf16_to_f32(A)[I - 1]
+    s = f[:, 0].copy()
+    for i in range(1, 20):
+        s += f[:, i]
+    assert np.array_equal(oracle.pooled_sum(A, I, bf16=True), oracle.f32_to_bf16(s))
+    assert np.array_equal(oracle.gather(A, I[:, 0], bf16=True), A[I[:, 0] - 1])
+    u = oracle.fill_uniform((1000,), "bf16", 5, 0, -1.0, 1.0)
+    assert np.array_equal(u, oracle.f32_to_bf16(oracle.fill_uniform((1000,), np.float32, 5, 0,
+                                                                     -1.0, 1.0)))
+
+
 def test_pool_zero_and_empty(oracle):
     A = np.ones((10, 16), np.float32)
     assert np.array_equal(oracle.pooled_sum(A, np.zeros((5, 0), np.int64)), np.zeros((5, 16)))
