@@ -244,7 +244,9 @@ struct UpdateDesc
     cols_per_page::Int64
 end
 
-function _update_desc(A::HipTable{S,Float32}, g::SparseEmbeddingUpdate) where {S}
+const UpdateEltype = Union{Float32,Float64,Float16}  # et_sparse_sgd's table types
+
+function _update_desc(A::HipTable{S,<:UpdateEltype}, g::SparseEmbeddingUpdate) where {S}
     dp, dld = _ptr_ld(g.delta)
     I = g.indices
     pool = ndims(I) == 1 ? 1 : size(I, 1)
@@ -268,22 +270,23 @@ function _workspace(nbytes)
     return ws
 end
 
-function _sparse_sgd(descs::Vector{UpdateDesc}, eta::Float64, flags::UInt32)
+function _sparse_sgd(::Type{T}, descs::Vector{UpdateDesc}, eta::Float64, flags::UInt32) where {T}
     nb = Ref{Int64}(0)
     check(ccall((:et_sgd_workspace_size, libembtab), Cint, (Ptr{UpdateDesc}, Int32, Ref{Int64}),
                 descs, length(descs), nb))
     ws = _workspace(nb[])
     check(ccall((:et_sparse_sgd, libembtab), Cint,
                 (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
-                ET_F32, descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
+                et_dtype(T), descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
 end
 
-function update!(opt::Flux.Descent, table::HipTable{S,Float32}, grad::SparseEmbeddingUpdate,
-                 indexer = Indexer(), ::Val{Nontemporal} = Val(true), args...) where {S,Nontemporal}
+function update!(opt::Flux.Descent, table::HipTable{S,T}, grad::SparseEmbeddingUpdate,
+                 indexer = Indexer(), ::Val{Nontemporal} = Val(true),
+                 args...) where {S,T<:UpdateEltype,Nontemporal}
     flags = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
             (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED)
-    # convert(eltype(table), opt.eta) happens inside the fp32 kernel
-    _sparse_sgd([_update_desc(table, grad)], Float64(opt.eta), flags)
+    # convert(eltype(table), opt.eta) happens inside the library
+    _sparse_sgd(T, [_update_desc(table, grad)], Float64(opt.eta), flags)
     return nothing
 end
 
@@ -293,14 +296,15 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  telemetry_cb = Returns(nothing), kw...) where {Nontemporal}
     telemetry_cb()
     nt = Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)
-    for fused in (true, false)
-        sel = [i for i in eachindex(tables) if _fused(tables[i]) == fused]
+    for fused in (true, false), T in (Float32, Float64, Float16)
+        sel = [i for i in eachindex(tables) if _fused(tables[i]) == fused &&
+                                               eltype(tables[i]) === T]
         isempty(sel) && continue
         # the multi-table generic path sees opt.eta as Float64 (src/sparseupdate.jl:232)
         flags = nt | (fused ? UInt32(0) : ET_FLAG_SGD_UNFUSED | ET_FLAG_SGD_F64_ALPHA)
         for chunk in Iterators.partition(sel, 32)
-            _sparse_sgd([_update_desc(tables[i], grads[i]) for i in chunk], Float64(opt.eta),
-                        flags)
+            _sparse_sgd(T, [_update_desc(tables[i], grads[i]) for i in chunk],
+                        Float64(opt.eta), flags)
         end
     end
     return nothing
