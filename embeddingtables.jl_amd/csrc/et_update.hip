@@ -132,16 +132,33 @@ __global__ __launch_bounds__(256) void k_seg_chunks(const uint32_t* __restrict__
     if (c > 1) mlist[atomicAdd(&counters[kCntM], 1u)] = (uint32_t)u;
 }
 
-__global__ __launch_bounds__(256) void k_chunk_seg(const uint32_t* __restrict__ chunk_start,
-                                                   const uint32_t* __restrict__ counters,
-                                                   int64_t n, uint32_t* __restrict__ chunk_seg,
-                                                   uint32_t* __restrict__ counters_out) {
+// One 16-byte record per chunk — its occurrence range, its column key and where its
+// sum goes (kApply: update the column directly; else its partial slot) — so the SGD
+// passes fetch a chunk's metadata with one load instead of a chain of dependent ones.
+struct ChunkRec {
+    uint32_t s0, s1, key, dst;
+};
+constexpr uint32_t kApply = 0xffffffffu;
+
+__global__ __launch_bounds__(256) void k_chunk_records(
+    const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ seg_start,
+    const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ keys,
+    uint32_t chunk, uint32_t* __restrict__ counters, ChunkRec* __restrict__ recs) {
     const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const uint32_t U = counters[kCntU];
-    if (u == 0) counters_out[kCntC] = chunk_start[U];
+    if (u == 0) counters[kCntC] = chunk_start[U];
     if (u >= U) return;
-    for (uint32_t c = chunk_start[u]; c < chunk_start[u + 1]; ++c) chunk_seg[c] = (uint32_t)u;
-    (void)n;
+    const uint32_t ss = seg_start[u], se = seg_start[u + 1], key = keys[ss];
+    const uint32_t cs = chunk_start[u], nc = chunk_start[u + 1] - cs;
+    if (nc == 1) {
+        recs[cs] = ChunkRec{ss, se, key, kApply};
+        return;
+    }
+    const uint32_t ps = partial_start[u];
+    for (uint32_t p = 0; p < nc; ++p) {
+        const uint32_t s0 = ss + p * chunk;
+        recs[cs + p] = ChunkRec{s0, s0 + chunk < se ? s0 + chunk : se, key, ps + p};
+    }
 }
 
 // 5./6. gradient sums and the update ---------------------------------------------
@@ -275,11 +292,9 @@ __device__ __forceinline__ void apply_row(float* __restrict__ w, const u32x4 (&x
 template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chunks(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
-    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ seg_start,
-    const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_seg,
-    const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ counters,
-    uint32_t chunk, float* __restrict__ partials, int pdim, uint32_t sent, float eta32,
-    double eta64) {
+    const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
+    const uint32_t* __restrict__ counters, float* __restrict__ partials, int pdim,
+    uint32_t sent, float eta32, double eta64) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -294,17 +309,9 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
         // metadata of chunks (it*64 + l) * nwaves + wid, one per lane l
         const uint64_t cl = ((uint64_t)it * 64u + lane) * nwaves + wid;
         const bool valid = cl < C;
-        const uint32_t c = valid ? (uint32_t)cl : C - 1;
-        const uint32_t u = chunk_seg[c];
-        const uint32_t cs = chunk_start[u], ce = chunk_start[u + 1];
-        const uint32_t ss = seg_start[u], se = seg_start[u + 1];
-        const uint32_t key = keys[ss];
-        const uint32_t ps = partial_start[u];
-        const uint32_t p = c - cs;
-        const uint32_t m_s0 = ss + p * chunk;
-        const uint32_t m_s1 = m_s0 + chunk < se ? m_s0 + chunk : se;
-        const uint32_t m_dst = (ce - cs == 1) ? 0xffffffffu : ps + p;
-        const uint32_t m_key = valid ? key : sent;
+        const ChunkRec r = recs[valid ? (uint32_t)cl : C - 1];
+        const uint32_t m_s0 = r.s0, m_s1 = r.s1, m_dst = r.dst;
+        const uint32_t m_key = valid ? r.key : sent;
         const uint64_t left = ((uint64_t)C - wid + nwaves - 1) / nwaves - (uint64_t)it * 64u;
         const uint32_t nq = left < 64u ? (uint32_t)left : 64u;
         for (uint32_t qq = 0; qq < nq; qq += GPW) {
@@ -440,25 +447,20 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
 template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
-    const uint32_t* __restrict__ vals, const uint32_t* __restrict__ seg_start,
-    const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ chunk_seg,
-    const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ counters,
-    uint32_t chunk, C* __restrict__ partials, int pdim, uint32_t sent, C eta_c, double eta64) {
+    const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
+    const uint32_t* __restrict__ counters, C* __restrict__ partials, int pdim, uint32_t sent,
+    C eta_c, double eta64) {
     const int lane = threadIdx.x & 63;
     const uint32_t Cn = counters[kCntC];
     const uint32_t waves = gridDim.x * 4;
     for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < Cn; c += waves) {
-        const uint32_t u = chunk_seg[c];
-        const uint32_t pidx = c - chunk_start[u];
-        const uint32_t nchunks = chunk_start[u + 1] - chunk_start[u];
-        const uint32_t seg0 = seg_start[u], seg1 = seg_start[u + 1];
-        const uint32_t key = keys[seg0];
+        const ChunkRec r = recs[c];
+        const uint32_t key = r.key;
         if (key == sent) continue;
         const int t = table_of_key(pack, ntables, key);
         const et_update_desc& d = pack.d[t];
         if ((pack.vec_mask >> t) & 1u) continue;  // handled by the vector kernel
-        const uint32_t s0 = seg0 + pidx * chunk;
-        const uint32_t s1 = s0 + chunk < seg1 ? s0 + chunk : seg1;
+        const uint32_t s0 = r.s0, s1 = r.s1;
         const T* delta = reinterpret_cast<const T*>(d.delta);
         for (int f = lane; f < d.dim; f += 64) {
             C acc = C(0);
@@ -466,11 +468,11 @@ __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
                 const uint32_t bag = (vals[o] - pack.occ_off[t]) / (uint32_t)d.pool;
                 acc = acc + C(delta[(uint64_t)bag * (uint64_t)d.ld_delta + f]);
             }
-            if (nchunks == 1) {
+            if (r.dst == kApply) {
                 T* w = col_ptr<T>(d.table, d.ld_table, d.cols_per_page, key - pack.row_off[t]) + f;
                 store_scalar<NT>(w, sgd_apply_t<T, C, MODE>(*w, acc, eta_c, eta64));
             } else {
-                partials[(uint64_t)(partial_start[u] + pidx) * pdim + f] = acc;
+                partials[(uint64_t)r.dst * pdim + f] = acc;
             }
         }
     }
@@ -507,8 +509,9 @@ __global__ __launch_bounds__(256) void k_sgd_combine_generic(
 // ---------------------------------------------------------------------------
 
 struct UpdateWs {
-    uint32_t *ka, *va, *kb, *vb, *hist, *part, *flag, *seg_start, *nch, *multi, *chunk_seg,
-        *counters, *mlist;
+    uint32_t *ka, *va, *kb, *vb, *hist, *part, *flag, *seg_start, *nch, *multi, *counters,
+        *mlist;
+    ChunkRec* recs;
     float* partials;
     int64_t bytes;
 };
@@ -539,7 +542,7 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk)
     w.nch = (uint32_t*)take(4 * (n1 + 1));
     w.multi = (uint32_t*)take(4 * (n1 + 1));
     const int64_t max_chunks = n + n / chunk + 2;
-    w.chunk_seg = (uint32_t*)take(4 * max_chunks);
+    w.recs = (ChunkRec*)take((int64_t)sizeof(ChunkRec) * max_chunks);
     w.counters = (uint32_t*)take(4 * kCntSlots);
     w.mlist = (uint32_t*)take(4 * (n / chunk + 2));
     const int64_t max_partials = 2 * (n / chunk) + 2;
@@ -604,9 +607,9 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     if (rc != ET_OK) return rc;
     rc = exclusive_scan_u32(w.multi, w.multi, n + 1, w.part, s);
     if (rc != ET_OK) return rc;
-    hipLaunchKernelGGL(k_chunk_seg, dim3((unsigned)blocks), dim3(256), 0, s, w.nch, w.counters, n,
-                       w.chunk_seg, w.counters);
-    ET_LAUNCH_CHECK("k_chunk_seg");
+    hipLaunchKernelGGL(k_chunk_records, dim3((unsigned)blocks), dim3(256), 0, s, w.nch,
+                       w.seg_start, w.multi, out.keys, chunk, w.counters, w.recs);
+    ET_LAUNCH_CHECK("k_chunk_records");
     return ET_OK;
 }
 
@@ -622,8 +625,8 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
 #define ET_SGD_VEC(DD)                                                                         \
     case DD:                                                                                   \
         hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
-                           ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg,         \
-                           w.multi, w.counters, chunk, w.partials, pdim, sent, eta_c, eta64);  \
+                           ntables, gr.keys, gr.vals, w.recs, w.counters, w.partials, pdim,    \
+                           sent, eta_c, eta64);                                                \
         hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,   \
                            ntables, gr.keys, w.seg_start, w.multi, w.counters, w.mlist,        \
                            w.partials, pdim, sent, eta_c, eta64);                              \
@@ -643,8 +646,8 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     if (any_generic) {
         C* partials = reinterpret_cast<C*>(w.partials);
         hipLaunchKernelGGL((k_sgd_chunks_generic<T, C, MODE, NT>), dim3(grid), dim3(256), 0, s,
-                           pack, ntables, gr.keys, gr.vals, w.seg_start, w.nch, w.chunk_seg,
-                           w.multi, w.counters, chunk, partials, pdim, sent, eta_c, eta64);
+                           pack, ntables, gr.keys, gr.vals, w.recs, w.counters, partials, pdim,
+                           sent, eta_c, eta64);
         hipLaunchKernelGGL((k_sgd_combine_generic<T, C, MODE, NT>), dim3(grid), dim3(256), 0, s,
                            pack, ntables, gr.keys, w.seg_start, w.multi, w.counters, partials,
                            pdim, sent, eta_c, eta64);
