@@ -158,3 +158,61 @@ def test_config4_full_size(oracle, criteo):
                 err = np.abs(got.astype(np.float64) - exact)
                 assert np.all(err <= 1e-6 * scale), (t, c, n, float((err / scale).max()))
                 assert err.max() <= np.abs(w[0].astype(np.float64) - exact).max(), (t, c, n)
+
+
+def test_config1_reference_plumbing(oracle):
+    """BASELINE config 1: SimpleEmbedding Float32 dim 16, 1000 columns, vector indices
+    B = 128 — the GPU result equals the oracle's and the reference's naive lookup."""
+    rng = np.random.default_rng(0)
+    h = rng.random((1000, 16), dtype=np.float32)
+    I = rng.integers(1, 1001, 128)
+    A = et.SimpleEmbedding(torch.from_numpy(h).to(DEV), et.Static(16))
+    got = et.lookup(A, torch.from_numpy(I).to(DEV)).cpu().numpy()
+    assert got.tobytes() == oracle.gather(h, I).tobytes() == oracle.naive_lookup(h, I).tobytes()
+
+
+def test_config5_shape_simulated_8_ranks(oracle):
+    """BASELINE config 5 shape (26 Criteo tables, B = 131072) through the 8-rank
+    feature-balanced plan on one GPU: every simulated rank looks up its pieces into
+    its slab with the real kernels; the stacked slabs are assembled by et_concat_slabs
+    (all-gather layout) or sliced per rank (all-to-all layout).  Both equal the
+    unsharded Preallocation output bit for bit."""
+    from embtab.sharding import ShardedMapLookup, ShardPlan, piece_table
+
+    Bc = 131072
+    L = _lib.load()
+    s = _lib.stream_handle()
+    tabs, idx = [], []
+    for t, R in enumerate(ROWS):
+        x = torch.empty((R, D), dtype=torch.float32, device=DEV)
+        _lib.check(L.et_fill_uniform(_lib.ET_F32, x.data_ptr(), x.numel(), 1000 + t, 0, 0.0, 1.0,
+                                     s))
+        I = torch.empty((Bc, P), dtype=torch.int64, device=DEV)
+        _lib.check(L.et_fill_index_uniform(I.data_ptr(), I.numel(), R, 5000 + t, 0, s))
+        tabs.append(et.SimpleEmbedding(x, et.Static(D)))
+        idx.append(I)
+    base = et.maplookup(et.PreallocationStrategy(), tabs, idx)
+    g = torch.Generator().manual_seed(5)
+    _sample_check(oracle, tabs, idx, base, torch.randint(0, Bc, (256,), generator=g).to(DEV))
+    world = 8
+    plan = ShardPlan.featurewise([D] * len(ROWS), world)
+    slabs = []
+    for r in range(world):
+        sm = ShardedMapLookup(plan, r, world, Bc, torch.float32, DEV)
+        ps = plan.pieces[r]
+        sm.lookup_chunk([piece_table(tabs[p.table], p) for p in ps], [idx[p.table] for p in ps],
+                        0, Bc)
+        slabs.append(sm.slab)
+    gathered = torch.stack(slabs)
+    dst = torch.empty_like(base)
+    sm.assemble_chunk(gathered, dst)
+    assert torch.equal(dst, base)
+    a2a = [ShardedMapLookup(plan, r, world, Bc, torch.float32, DEV, exchange="alltoall")
+           for r in range(world)]
+    for r in (0, 5):
+        lo, hi = a2a[r].split[r], a2a[r].split[r + 1]
+        part = torch.empty((hi - lo, plan.ld), dtype=torch.float32, device=DEV)
+        a2a[r].assemble_chunk(gathered[:, lo:hi].contiguous(), part)
+        assert torch.equal(part, base[lo:hi])
+    del tabs, idx, base, slabs, gathered, dst
+    torch.cuda.empty_cache()
