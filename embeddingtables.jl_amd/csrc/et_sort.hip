@@ -48,11 +48,26 @@ __device__ __forceinline__ uint32_t block_inclusive_scan_256(uint32_t v, uint32_
     return v + off;
 }
 
+// `mlen` (optional, device): the scan covers min(m, *mlen + madd) elements — a length
+// only known on the device (e.g. the number of segments); tiles beyond it do nothing.
+__device__ __forceinline__ int64_t scan_len(int64_t m, const uint32_t* mlen, uint32_t madd) {
+    if (!mlen) return m;
+    const int64_t l = (int64_t)*mlen + madd;
+    return l < m ? l : m;
+}
+
 __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t* __restrict__ in,
                                                               int64_t m,
-                                                              uint32_t* __restrict__ part) {
+                                                              uint32_t* __restrict__ part,
+                                                              const uint32_t* __restrict__ mlen,
+                                                              uint32_t madd) {
     __shared__ uint32_t lds4[4];
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    m = scan_len(m, mlen, madd);
+    if (base >= m) {
+        if (threadIdx.x == 0) part[blockIdx.x] = 0;
+        return;
+    }
     uint32_t s = 0;
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
@@ -83,10 +98,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_partials(uint32_t* __rest
 // Blocked per-thread segments: thread t scans elements [t*16, t*16+16) of the tile.
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(const uint32_t* __restrict__ in,
                                                             uint32_t* __restrict__ out, int64_t m,
-                                                            const uint32_t* __restrict__ part) {
+                                                            const uint32_t* __restrict__ part,
+                                                            const uint32_t* __restrict__ mlen,
+                                                            uint32_t madd) {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t tile[kScanTile + kScanTile / 32];
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    m = scan_len(m, mlen, madd);
+    if (base >= m) return;
     // striped, coalesced load into LDS (padded every 32 words against bank conflicts)
 #pragma unroll
     for (int r = 0; r < kScanItems; ++r) {
@@ -123,15 +142,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const uint32_t* __re
 
 // Exclusive scan of m (< 2^32 total) uint32 values; out may alias in.  out[m] is NOT
 // written; the total is left in part[np].  `part` needs cdiv(m, 4096) + 1 entries.
+// With `mlen`, only the first min(m, *mlen + madd) elements (a device-side length) are
+// scanned and written.
 inline int exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t m, uint32_t* part,
-                              hipStream_t s) {
+                              hipStream_t s, const uint32_t* mlen = nullptr,
+                              uint32_t madd = 0) {
     if (m <= 0) return ET_OK;
     const int64_t np = cdiv64(m, kScanTile);
     if (np > 0x7fffffffll) return fail(ET_ERR_ARG, "scan too large");
-    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, m, part);
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, m, part,
+                       mlen, madd);
     hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, part, np);
     hipLaunchKernelGGL(k_scan_down, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, out, m,
-                       part);
+                       part, mlen, madd);
     ET_LAUNCH_CHECK("exclusive_scan_u32");
     return ET_OK;
 }

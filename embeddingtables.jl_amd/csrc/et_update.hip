@@ -120,8 +120,8 @@ __global__ __launch_bounds__(256) void k_seg_chunks(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ multi,
                                                     uint32_t* __restrict__ mlist) {
     const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (u > n) return;
     const uint32_t U = counters[kCntU];
+    if (u > n || u > U) return;  // entries 0..U only: the scans below stop at U + 1
     uint32_t c = 0;
     if (u < U) {
         const uint32_t len = seg_start[u + 1] - seg_start[u];
@@ -603,9 +603,9 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
                        w.counters, chunk, w.nch, w.multi, w.mlist);
     ET_LAUNCH_CHECK("k_seg_chunks");
     // nch -> chunk_start, multi -> partial_start (in place, n+1 entries)
-    rc = exclusive_scan_u32(w.nch, w.nch, n + 1, w.part, s);
+    rc = exclusive_scan_u32(w.nch, w.nch, n + 1, w.part, s, w.counters + kCntU, 1);
     if (rc != ET_OK) return rc;
-    rc = exclusive_scan_u32(w.multi, w.multi, n + 1, w.part, s);
+    rc = exclusive_scan_u32(w.multi, w.multi, n + 1, w.part, s, w.counters + kCntU, 1);
     if (rc != ET_OK) return rc;
     hipLaunchKernelGGL(k_chunk_records, dim3((unsigned)blocks), dim3(256), 0, s, w.nch,
                        w.seg_start, w.multi, out.keys, chunk, w.counters, w.recs);
