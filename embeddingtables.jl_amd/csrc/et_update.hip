@@ -88,26 +88,65 @@ __global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg,
 }
 
 // 3. segments ------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_seg_flags(const uint32_t* __restrict__ keys, int64_t n,
-                                                   uint32_t* __restrict__ flag) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+// Segment starts = stream compaction of the head flags (key differs from the previous
+// one), fused into a tile scan: k_seg_reduce counts heads per 4096-key tile,
+// k_scan_partials scans the tile counts, k_seg_down recomputes the flags of its tile,
+// scans them and writes seg_start[segment] = position (and U, seg_start[U] = n).
+__device__ __forceinline__ uint32_t seg_head(const uint32_t* __restrict__ keys, int64_t i) {
+    return (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
 }
 
-// flag (as read) / segid (exclusive scan of flag) -> seg_start, U.
-__global__ __launch_bounds__(256) void k_seg_start(const uint32_t* __restrict__ keys,
-                                                   const uint32_t* __restrict__ segid, int64_t n,
-                                                   uint32_t* __restrict__ seg_start,
-                                                   uint32_t* __restrict__ counters) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const bool head = (i == 0 || keys[i] != keys[i - 1]);
-    if (head) seg_start[segid[i]] = (uint32_t)i;
-    if (i == n - 1) {
-        // segid is the EXCLUSIVE scan of the head flags: U = heads before + this head
-        const uint32_t U = segid[i] + (head ? 1u : 0u);
-        seg_start[U] = (uint32_t)n;
-        counters[kCntU] = U;
+__global__ __launch_bounds__(kScanThreads) void k_seg_reduce(const uint32_t* __restrict__ keys,
+                                                             int64_t n,
+                                                             uint32_t* __restrict__ part) {
+    __shared__ uint32_t lds4[4];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    uint32_t h = 0;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {
+        const int64_t i = base + r * kScanThreads + threadIdx.x;
+        if (i < n) h += seg_head(keys, i);
+    }
+    uint32_t total;
+    block_inclusive_scan_256(h, lds4, &total);
+    if (threadIdx.x == 0) part[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_seg_down(const uint32_t* __restrict__ keys,
+                                                           int64_t n,
+                                                           const uint32_t* __restrict__ part,
+                                                           uint32_t* __restrict__ seg_start,
+                                                           uint32_t* __restrict__ counters) {
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t tile[kScanTile + kScanTile / 32];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+#pragma unroll
+    for (int r = 0; r < kScanItems; ++r) {  // striped, coalesced
+        const int e = r * kScanThreads + threadIdx.x;
+        const int64_t i = base + e;
+        tile[e + (e >> 5)] = i < n ? seg_head(keys, i) : 0u;
+    }
+    __syncthreads();
+    uint32_t v[kScanItems];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int e = threadIdx.x * kScanItems + k;
+        v[k] = tile[e + (e >> 5)];
+        sum += v[k];
+    }
+    uint32_t total;
+    const uint32_t inc = block_inclusive_scan_256(sum, lds4, &total);
+    uint32_t run = part[blockIdx.x] + inc - sum;  // exclusive prefix of this thread's run
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int64_t i = base + threadIdx.x * kScanItems + k;
+        if (i < n && v[k]) seg_start[run] = (uint32_t)i;
+        run += v[k];
+        if (i == n - 1) {  // U = heads up to and including the last key
+            seg_start[run] = (uint32_t)n;
+            counters[kCntU] = run;
+        }
     }
 }
 
@@ -509,7 +548,7 @@ __global__ __launch_bounds__(256) void k_sgd_combine_generic(
 // ---------------------------------------------------------------------------
 
 struct UpdateWs {
-    uint32_t *ka, *va, *kb, *vb, *hist, *part, *flag, *seg_start, *nch, *multi, *counters,
+    uint32_t *ka, *va, *kb, *vb, *hist, *part, *seg_start, *nch, *multi, *counters,
         *mlist;
     ChunkRec* recs;
     float* partials;
@@ -537,7 +576,6 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk)
     w.vb = (uint32_t*)take(4 * n1);
     w.hist = (uint32_t*)take(4 * hist_m);
     w.part = (uint32_t*)take(4 * scan_part_entries(scan_m));
-    w.flag = (uint32_t*)take(4 * (n1 + 1));
     w.seg_start = (uint32_t*)take(4 * (n1 + 1));
     w.nch = (uint32_t*)take(4 * (n1 + 1));
     w.multi = (uint32_t*)take(4 * (n1 + 1));
@@ -590,14 +628,15 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     SortBuffers sb{w.ka, w.va, w.kb, w.vb, w.hist, w.part};
     int rc = segmented_radix_sort(sb, seg, ntables, &out.keys, &out.vals, s);
     if (rc != ET_OK) return rc;
-    hipLaunchKernelGGL(k_seg_flags, dim3((unsigned)blocks), dim3(256), 0, s, out.keys, n, w.flag);
-    ET_LAUNCH_CHECK("k_seg_flags");
-    // flag -> segment id (in place)
-    rc = exclusive_scan_u32(w.flag, w.flag, n, w.part, s);
-    if (rc != ET_OK) return rc;
-    hipLaunchKernelGGL(k_seg_start, dim3((unsigned)blocks), dim3(256), 0, s, out.keys, w.flag, n,
-                       w.seg_start, w.counters);
-    ET_LAUNCH_CHECK("k_seg_start");
+    {
+        const int64_t np = cdiv64(n, kScanTile);
+        hipLaunchKernelGGL(k_seg_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, out.keys,
+                           n, w.part);
+        hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, w.part, np);
+        hipLaunchKernelGGL(k_seg_down, dim3((unsigned)np), dim3(kScanThreads), 0, s, out.keys,
+                           n, w.part, w.seg_start, w.counters);
+        ET_LAUNCH_CHECK("k_seg_down");
+    }
     const int64_t blocks1 = cdiv64(n + 1, 256);
     hipLaunchKernelGGL(k_seg_chunks, dim3((unsigned)blocks1), dim3(256), 0, s, w.seg_start, n,
                        w.counters, chunk, w.nch, w.multi, w.mlist);
