@@ -398,7 +398,9 @@ def main():
                 shard.lookup_chunk(tables, idx, shard.bounds[c], shard.bounds[c + 1])
             ev[k][1].record(stream)
         torch.cuda.synchronize()
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kernel_times = sorted(a.elapsed_time(b) for a, b in ev)
+    kernel_ms = sum(kernel_times) / args.steps
+    kernel_ms_median = kernel_times[len(kernel_times) // 2]
 
     lookups_per_step = B * T * POOL
     value = lookups_per_step * args.steps / elapsed
@@ -449,6 +451,7 @@ def main():
             "traffic": traffic_bytes,
             "algorithmic_bytes_per_launch": local_bytes,
             "kernel_ms": kernel_ms,
+            "kernel_ms_median": kernel_ms_median,
         },
     }
     if sharded:
@@ -457,6 +460,14 @@ def main():
         if world > 1 and not args.no_alltoall:
             result["alltoall"] = bench_alltoall(plan, rank, world, B, device, tables, idx,
                                                 max(5, args.steps // 2), 2)
+    if world == 1 and not args.no_extra and not sharded:
+        # config 3 also at prependrows k = 16 (dst ld = 16 + 3328)
+        dst16 = torch.empty((B, 16 + sum(dims)), dtype=torch.float32, device=device)
+        ms16 = _timed(lambda: et.maplookup_(et.PreallocationStrategy(16), dst16, tables, idx),
+                      max(10, args.steps // 2), 2, stream)
+        result["config3_prepend16"] = {"kernel_ms": ms16,
+                                       "lookups_per_s": lookups_per_step / (ms16 * 1e-3)}
+        del dst16
     if world == 1 and not args.no_extra:
         result["config2_gather"] = bench_config2(et, L, device, 200, 10)
         result["config4_zipf_update"] = bench_config4(et, tables, mine, device, 10, 2, B)
