@@ -99,12 +99,16 @@ __device__ __forceinline__ long long load_idx_chunk(const int64_t* __restrict__ 
 // PG (paged table, SplitEmbedding): `table` is the device array of page pointers and
 // column r lives in page r / cpp at column r % cpp; the UU page-pointer loads are
 // issued together before the row loads.
-template <typename T, typename A, int D, int UU, bool NTL, bool PG = false>
+//
+// MK (masked geometry): D is a power-of-two CAPACITY and the table's rows have only
+// `vpr` 16-byte vectors (any dim that is a multiple of 16 bytes); lanes beyond the row
+// re-read its last vector (same cache line, never out of bounds) and never store.
+template <typename T, typename A, int D, int UU, bool NTL, bool PG = false, bool MK = false>
 __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t ld_table,
                                          uint32_t nrows, uint32_t cpp, long long my, int g,
                                          int sub, int i0, bool first_batch,
                                          A (&acc)[VecGeom<T, D>::NV][VecGeom<T, D>::N],
-                                         int& bad) {
+                                         int& bad, int vpr) {
     using G = VecGeom<T, D>;
     constexpr int N = G::N, LPR = G::LPR, NV = G::NV;
     uint64_t off[UU];
@@ -125,16 +129,22 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t l
             base[u] = table;
         }
     }
+    int vix[NV];  // this lane's vector of the row for each v
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        vix[v] = sub + v * LPR;
+        if constexpr (MK) vix[v] = vix[v] < vpr ? vix[v] : vpr - 1;
+    }
     u32x4 buf[UU][NV];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const u32x4* src = reinterpret_cast<const u32x4*>(base[u] + off[u]) + sub;
+        const u32x4* src = reinterpret_cast<const u32x4*>(base[u] + off[u]);
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             if constexpr (NTL)
-                buf[u][v] = __builtin_nontemporal_load(src + v * LPR);
+                buf[u][v] = __builtin_nontemporal_load(src + vix[v]);
             else
-                buf[u][v] = src[v * LPR];
+                buf[u][v] = src[vix[v]];
         }
     }
 #pragma unroll
@@ -162,12 +172,13 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t l
 // Accumulation is acc = row(I[1]); acc += row(I[i]) for i = 2..P, element-wise and in
 // order (src/lookup.jl:139-146), so fp32/fp64/int results equal the reference bit
 // for bit; F16 rounds after every add (Julia Float16 `+`) unless A = float.
-template <typename T, typename A, int D, int U, bool NT, bool NTL, bool PG = false>
+template <typename T, typename A, int D, int U, bool NT, bool NTL, bool PG = false,
+          bool MK = false>
 __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_t ld_table,
                                             uint32_t nrows, uint32_t cpp,
                                             const int64_t* __restrict__ ip,
                                             int pool, long long my0, T* __restrict__ out, int g,
-                                            int sub) {
+                                            int sub, int vpr) {
     using G = VecGeom<T, D>;
     constexpr int N = G::N, LPR = G::LPR, NV = G::NV;
     A acc[NV][N];
@@ -182,8 +193,8 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_
         const long long my = c0 == 0 ? my0 : load_idx_chunk<LPR>(ip + c0, cnt, sub);
         int i0 = 0;
 #define ET_LOAD_ADD(UU) \
-    load_add<T, A, D, UU, NTL, PG>(table, ld_table, nrows, cpp, my, g, sub, i0, c0 + i0 == 0, \
-                                   acc, bad)
+    load_add<T, A, D, UU, NTL, PG, MK>(table, ld_table, nrows, cpp, my, g, sub, i0,        \
+                                       c0 + i0 == 0, acc, bad, vpr)
         for (; i0 + U <= cnt; i0 += U) ET_LOAD_ADD(U);
         if constexpr (U > 8) {
             if (cnt - i0 >= 8) {
@@ -213,14 +224,14 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_
         T y[N];
 #pragma unroll
         for (int k = 0; k < N; ++k) y[k] = T(acc[v][k]);
-        store16<NT>(o + v * LPR, pack16<T, N>(y));
+        if (!MK || sub + v * LPR < vpr) store16<NT>(o + v * LPR, pack16<T, N>(y));
     }
 }
 
 // `rounds` bags of one table per lane group, the next bag's first index chunk loaded
 // while the current bag's rows are in flight.
 template <typename T, typename A, int D, int U, bool NT, bool NTL, bool NTI = false,
-          bool PG = false>
+          bool PG = false, bool MK = false>
 __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
                                          T* __restrict__ dst, int64_t ld_dst, int64_t chunk,
                                          int rounds) {
@@ -232,6 +243,7 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
     const int pool = d.pool;
     const int cnt0 = pool < G::LPR ? pool : G::LPR;
     const uint32_t ldt = (uint32_t)d.ld_table, nr = (uint32_t)d.nrows;
+    const int vpr = MK ? d.dim / G::N : G::VPR;  // vectors per row
     int64_t bag = chunk * per_round * rounds + wave * G::GPW + g;
     long long my_next = load_idx_chunk<G::LPR, NTI>(
         d.idx + (bag < batch ? bag : batch - 1) * d.ld_idx, cnt0, sub);
@@ -242,22 +254,22 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
         if (r + 1 < rounds)
             my_next = load_idx_chunk<G::LPR, NTI>(
                 d.idx + (nbag < batch ? nbag : batch - 1) * d.ld_idx, cnt0, sub);
-        bag_sum_vec<T, A, D, U, NT, NTL, PG>(table, ldt, nr, (uint32_t)d.cols_per_page,
-                                             d.idx + bag * d.ld_idx, pool, my,
-                                         dst + bag * ld_dst + d.dst_row_off, g, sub);
+        bag_sum_vec<T, A, D, U, NT, NTL, PG, MK>(table, ldt, nr, (uint32_t)d.cols_per_page,
+                                                 d.idx + bag * d.ld_idx, pool, my,
+                                                 dst + bag * ld_dst + d.dst_row_off, g, sub, vpr);
         bag = nbag;
     }
 }
 
 // Pooled-sum kernel, vector path: grid = ntables * nchunks workgroups of 256.
-template <typename T, typename A, int D, int U, bool NT, bool PG = false>
+template <typename T, typename A, int D, int U, bool NT, bool PG = false, bool MK = false>
 __global__ __launch_bounds__(256) void k_pooled_vec(LookupPack pack, int ntables, int64_t batch,
                                                     T* __restrict__ dst, int64_t ld_dst,
                                                     int rounds) {
     const int64_t item = blockIdx.x;
     const int t = (int)(item % ntables);
     const int64_t chunk = item / ntables;
-    run_bags<T, A, D, U, NT, false, false, PG>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    run_bags<T, A, D, U, NT, false, false, PG, MK>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
 }
 
 // XCD-aware stripe schedule for multi-table launches.  Every table's chunks are cut
@@ -509,7 +521,7 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
     }
 }
 
-template <typename T, typename A, int D, int U, bool NT, bool PG = false>
+template <typename T, typename A, int D, int U, bool NT, bool PG = false, bool MK = false>
 int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                         hipStream_t s);
 
@@ -529,7 +541,7 @@ int launch_pooled_vec(const LookupPack& pack, int n, int64_t batch, void* dst, i
     return launch_pooled_vec_u<T, A, D, VecGeom<T, D>::U, NT>(pack, n, batch, dst, ld_dst, s);
 }
 
-template <typename T, typename A, int D, int U, bool NT, bool PG>
+template <typename T, typename A, int D, int U, bool NT, bool PG, bool MK>
 int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                         hipStream_t s) {
     using G = VecGeom<T, D>;
@@ -537,7 +549,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     const int rounds = rounds_for(batch, per_round, n);
     const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
     if (nchunks <= 0) return ET_OK;
-    if (!PG && n > 1 && tuning().striped) {
+    if (!PG && !MK && n > 1 && tuning().striped) {
         StripeMap sm;
         build_stripe_map(pack, n, (int)sizeof(T), sm);
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
@@ -557,7 +569,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     const int64_t grid = nchunks * n;
     if (grid <= 0) return ET_OK;
     if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
-    hipLaunchKernelGGL((k_pooled_vec<T, A, D, U, NT, PG>), dim3((unsigned)grid), dim3(256), 0, s,
+    hipLaunchKernelGGL((k_pooled_vec<T, A, D, U, NT, PG, MK>), dim3((unsigned)grid), dim3(256), 0, s,
                        pack, n, batch, reinterpret_cast<T*>(dst), ld_dst, rounds);
     ET_LAUNCH_CHECK("k_pooled_vec");
     return ET_OK;
@@ -612,6 +624,37 @@ int launch_pooled_dim(const LookupPack& pack, int n, int D, int64_t batch, void*
     return fail(ET_ERR_UNSUPPORTED, "vector dim %d", D);
 }
 
+// Dims that are a multiple of 16 bytes but not a power-of-two vector width: the masked
+// vector kernel at the next power-of-two capacity (up to 2048 elements).
+inline int masked_capacity(int D) {
+    int c = 16;
+    while (c < D) c <<= 1;
+    return c;
+}
+
+template <typename T, typename A, bool NT>
+int launch_pooled_masked(const LookupPack& pack, int n, int D, int64_t batch, void* dst,
+                         int64_t ld_dst, hipStream_t s) {
+#define ET_MK(C)                                                                              \
+    case C:                                                                                   \
+        if constexpr (C / (16 / (int)sizeof(T)) >= 1)                                         \
+            return launch_pooled_vec_u<T, A, C, VecGeom<T, C>::U, NT, false, true>(           \
+                pack, n, batch, dst, ld_dst, s);                                              \
+        break;
+    switch (masked_capacity(D)) {
+        ET_MK(16)
+        ET_MK(32)
+        ET_MK(64)
+        ET_MK(128)
+        ET_MK(256)
+        ET_MK(512)
+        ET_MK(1024)
+        ET_MK(2048)
+    }
+#undef ET_MK
+    return fail(ET_ERR_UNSUPPORTED, "masked vector dim %d", D);
+}
+
 template <typename T, typename A, bool NT>
 int launch_generic(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                    hipStream_t s) {
@@ -625,7 +668,7 @@ int launch_generic(const LookupPack& pack, int n, int64_t batch, void* dst, int6
 }
 
 // Kinds of launch group.
-enum GroupKind { kGather = 0, kPooledVec = 1, kGeneric = 2, kPagedVec = 3 };
+enum GroupKind { kGather = 0, kPooledVec = 1, kGeneric = 2, kPagedVec = 3, kMaskedVec = 4 };
 
 template <typename T, typename A, bool NT>
 int launch_group_typed(GroupKind kind, const LookupPack& pack, int n, int D, int64_t batch,
@@ -636,6 +679,8 @@ int launch_group_typed(GroupKind kind, const LookupPack& pack, int n, int D, int
     if (kind == kPooledVec) return launch_pooled_dim<T, A, NT>(pack, n, D, batch, dst, ld_dst, s);
     if (kind == kPagedVec)
         return launch_pooled_dim<T, A, NT, true>(pack, n, D, batch, dst, ld_dst, s);
+    if (kind == kMaskedVec)
+        return launch_pooled_masked<T, A, NT>(pack, n, D, batch, dst, ld_dst, s);
     return launch_generic<T, A, NT>(pack, n, batch, dst, ld_dst, s);
 }
 
@@ -718,6 +763,9 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
         } else if (d.pool >= 1 && al && vec_dim_ok(d.dim) && d.nrows < 0xffffffffll &&
                    d.ld_table < 0xffffffffll) {
             kind_of[t] = kPooledVec;
+        } else if (d.pool >= 1 && al && ((int64_t)d.dim * es) % 16 == 0 && d.dim <= 2048 &&
+                   d.nrows < 0xffffffffll && d.ld_table < 0xffffffffll) {
+            kind_of[t] = kMaskedVec;  // any other 16-byte-multiple row (96, 200, 1504 ...)
         } else {
             kind_of[t] = kGeneric;
         }

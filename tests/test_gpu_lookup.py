@@ -71,6 +71,53 @@ def test_lookup_parity(oracle, dim, static):
         assert bits_equal(host(et.lookup(A, dev(I))), oracle.lookup(h, I))
 
 
+@pytest.mark.parametrize("dim", [20, 24, 36, 48, 96, 200, 384, 1000, 2048])
+def test_masked_vector_dims(oracle, dim):
+    """Dims that are a multiple of 16 bytes but not a power-of-two vector width run the
+    masked vector kernel (next power-of-two capacity): bit-identical to the oracle for
+    pooled sums (pool 1, 12, 45), gathers, a strided destination and bad indices."""
+    rng = np.random.default_rng(dim)
+    h = rng.standard_normal((700, dim)).astype(np.float32)
+    A = table(h)
+    for I in (rng.integers(1, 701, (300, 12)), rng.integers(1, 701, (77, 45)),
+              rng.integers(1, 701, (64, 1))):
+        assert bits_equal(host(et.lookup(A, dev(I))), oracle.pooled_sum(h, I))
+    v = rng.integers(1, 701, 257)
+    assert bits_equal(host(et.lookup(A, dev(v))), oracle.gather(h, v))
+    I = rng.integers(1, 701, (100, 20))
+    big = torch.full((100, dim + 12), -3.0, dtype=torch.float32, device=DEV)
+    et.lookup_(big[:, 4:4 + dim], A, dev(I))
+    got = host(big)
+    assert bits_equal(got[:, 4:4 + dim], oracle.pooled_sum(h, I))
+    assert (got[:, :4] == -3.0).all() and (got[:, 4 + dim:] == -3.0).all()
+    et.check_errors()
+    bad = I.copy()
+    bad[3, 5] = 701
+    out = host(et.lookup(A, dev(bad)))
+    assert et.check_errors() == 1
+    ref = oracle.pooled_sum(h, I)
+    ref[3] = oracle.pooled_sum(h, np.delete(I[3:4], 5, axis=1))[0]
+    assert bits_equal(out, ref)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float16, np.int64, "bf16"])
+def test_masked_dims_other_types_and_mixed_launch(oracle, dtype):
+    rng = np.random.default_rng(5)
+    dims = [24, 40, 200, 128, 96]
+    hs = []
+    for d in dims:
+        x = rng.standard_normal((300, d)) * 50
+        hs.append(oracle.f32_to_bf16(x.astype(np.float32)) if dtype == "bf16"
+                  else x.astype(dtype))
+    hidx = [rng.integers(1, 301, (150, 16)) for _ in dims]
+    tabs = [et.SimpleEmbedding(dev(h).view(torch.bfloat16) if dtype == "bf16" else dev(h))
+            for h in hs]
+    out = et.maplookup(et.PreallocationStrategy(1), tabs, [dev(i) for i in hidx])
+    got = host(out.view(torch.int16)).view(np.uint16) if dtype == "bf16" else host(out)
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=1, bf16=dtype == "bf16")
+    assert bits_equal(got[:, 1:], ref[:, 1:])
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.int32, np.int64, np.float16])
 @pytest.mark.parametrize("dim", [16, 128, 40])
 def test_lookup_dtypes(oracle, dtype, dim):
