@@ -257,15 +257,30 @@ __device__ __forceinline__ uint32_t group_pick(uint32_t v, int base, int g) {
 // lane by lane and keeps U column loads in flight.  The groups of a wave walk chunks
 // of different lengths, so loop counters are NOT wave-uniform here: the broadcast is a
 // ds_bpermute (per-lane source index), never a readlane.
+//
+// D is the power-of-two capacity of the row; the table's rows have `vpr` <= D/4 16-byte
+// vectors (any dim that is a multiple of 4): lanes past the row re-read its last
+// vector (vec_index) and never store.
+template <int LPR, int NV>
+__device__ __forceinline__ void vec_index(int sub, int vpr, int (&vix)[NV]) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int i = sub + v * LPR;
+        vix[v] = i < vpr ? i : vpr - 1;
+    }
+}
+
 template <int D, int U>
 __device__ __forceinline__ void occ_sum(const float* __restrict__ delta, uint32_t ld_delta,
                                         uint32_t occ_off, uint32_t pool,
                                         const uint32_t* __restrict__ vals, uint32_t s0,
-                                        uint32_t s1, int g, int sub,
+                                        uint32_t s1, int g, int sub, int vpr,
                                         float (&acc)[(D / 4 < 64 ? 1 : D / 4 / 64)][4]) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
+    int vix[NV];
+    vec_index<LPR, NV>(sub, vpr, vix);
     for (uint32_t c0 = s0; c0 < s1; c0 += LPR) {
         const int cnt = (int)(s1 - c0 < (uint32_t)LPR ? s1 - c0 : (uint32_t)LPR);
         const uint32_t myo = vals[c0 + (uint32_t)(sub < cnt ? sub : cnt - 1)];
@@ -282,9 +297,9 @@ __device__ __forceinline__ void occ_sum(const float* __restrict__ delta, uint32_
             u32x4 buf[U][NV];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const u32x4* src = reinterpret_cast<const u32x4*>(delta + off[u]) + sub;
+                const u32x4* src = reinterpret_cast<const u32x4*>(delta + off[u]);
 #pragma unroll
-                for (int v = 0; v < NV; ++v) buf[u][v] = src[v * LPR];
+                for (int v = 0; v < NV; ++v) buf[u][v] = src[vix[v]];
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -304,9 +319,10 @@ __device__ __forceinline__ void occ_sum(const float* __restrict__ delta, uint32_
 }
 
 template <int D, int MODE, bool NT>
-__device__ __forceinline__ void apply_row(float* __restrict__ w, const u32x4 (&x)[(D / 4 < 64 ? 1 : D / 4 / 64)],
+__device__ __forceinline__ void apply_row(float* __restrict__ w,
+                                          const u32x4 (&x)[(D / 4 < 64 ? 1 : D / 4 / 64)],
                                           const float (&acc)[(D / 4 < 64 ? 1 : D / 4 / 64)][4],
-                                          int sub, float eta32, double eta64) {
+                                          int sub, int vpr, float eta32, double eta64) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -318,7 +334,7 @@ __device__ __forceinline__ void apply_row(float* __restrict__ w, const u32x4 (&x
         y.y = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x[v].y), acc[v][1], eta32, eta64));
         y.z = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x[v].z), acc[v][2], eta32, eta64));
         y.w = __float_as_uint(sgd_apply<MODE>(__uint_as_float(x[v].w), acc[v][3], eta32, eta64));
-        store16<NT>(wp + v * LPR, y);
+        if (sub + v * LPR < vpr) store16<NT>(wp + v * LPR, y);
     }
 }
 
@@ -364,25 +380,29 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
             if (!((pack.vec_mask >> t) & 1u)) continue;  // the generic kernels' table
             float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
                                       kkey - pack.row_off[t]);
+            const int vpr = d.dim / 4;
+            int vix[NV];
+            vec_index<LPR, NV>(sub, vpr, vix);
             u32x4 x[NV];
             if (dsl == 0xffffffffu) {
-                const u32x4* wp = reinterpret_cast<const u32x4*>(w) + sub;
+                const u32x4* wp = reinterpret_cast<const u32x4*>(w);
 #pragma unroll
-                for (int v = 0; v < NV; ++v) x[v] = wp[v * LPR];
+                for (int v = 0; v < NV; ++v) x[v] = wp[vix[v]];
             }
             float acc[NV][4];
 #pragma unroll
             for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
             occ_sum<D, U>(reinterpret_cast<const float*>(d.delta), (uint32_t)d.ld_delta,
-                          pack.occ_off[t], (uint32_t)d.pool, vals, s0, s1, g, sub, acc);
+                          pack.occ_off[t], (uint32_t)d.pool, vals, s0, s1, g, sub, vpr, acc);
             if (dsl == 0xffffffffu) {
-                apply_row<D, MODE, NT>(w, x, acc, sub, eta32, eta64);
+                apply_row<D, MODE, NT>(w, x, acc, sub, vpr, eta32, eta64);
             } else {
                 u32x4* pp = reinterpret_cast<u32x4*>(partials + (uint64_t)dsl * pdim) + sub;
 #pragma unroll
                 for (int v = 0; v < NV; ++v)
-                    pp[v * LPR] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
-                                        __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
+                    if (sub + v * LPR < vpr)
+                        pp[v * LPR] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
+                                            __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
             }
         }
     }
@@ -418,6 +438,9 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
                     continue;  // uniform across the workgroup
             }
             const uint32_t p0 = partial_start[seg], np = partial_start[seg + 1] - p0;
+            const int vpr = pack.d[table_of_key(pack, ntables, keys[seg_start[seg]])].dim / 4;
+            int vix[NV];
+            vec_index<LPR, NV>(sub, vpr, vix);
             const uint32_t a = p0 + (uint32_t)((uint64_t)np * G / NG);
             const uint32_t b = p0 + (uint32_t)((uint64_t)np * (G + 1) / NG);
             float acc[NV][4];
@@ -428,9 +451,9 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
 #pragma unroll
                 for (int uu = 0; uu < U; ++uu) {
                     const uint32_t q = q0 + uu < b ? q0 + uu : b - 1;
-                    const u32x4* pp = reinterpret_cast<const u32x4*>(partials + (uint64_t)q * pdim) + sub;
+                    const u32x4* pp = reinterpret_cast<const u32x4*>(partials + (uint64_t)q * pdim);
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) buf[uu][v] = pp[v * LPR];
+                    for (int v = 0; v < NV; ++v) buf[uu][v] = pp[vix[v]];
                 }
 #pragma unroll
                 for (int uu = 0; uu < U; ++uu) {
@@ -470,10 +493,10 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
                 float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
                                           key - pack.row_off[t]);
                 u32x4 x[NV];
-                const u32x4* wp = reinterpret_cast<const u32x4*>(w) + sub;
+                const u32x4* wp = reinterpret_cast<const u32x4*>(w);
 #pragma unroll
-                for (int v = 0; v < NV; ++v) x[v] = wp[v * LPR];
-                apply_row<D, MODE, NT>(w, x, tot, sub, eta32, eta64);
+                for (int v = 0; v < NV; ++v) x[v] = wp[vix[v]];
+                apply_row<D, MODE, NT>(w, x, tot, sub, vpr, eta32, eta64);
             }
             __syncthreads();
         }
@@ -677,6 +700,8 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
             ET_SGD_VEC(128)
             ET_SGD_VEC(256)
             ET_SGD_VEC(512)
+            ET_SGD_VEC(1024)
+            ET_SGD_VEC(2048)
             default: break;
         }
 #undef ET_SGD_VEC
@@ -816,12 +841,14 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         oo += (uint32_t)(d.pool * d.batch);
         if (d.pool == 0 || d.batch == 0 || d.dim == 0) continue;
         // paged tables qualify too: their pages are 16-byte aligned by contract
+        // vector kernels at the power-of-two capacity of the dim (masked below it)
+        const int cap = et::vec_dim_ok(d.dim) ? d.dim : et::masked_capacity(d.dim);
         const bool vec_ok = dtype == ET_F32 && (d.cols_per_page > 0 || et::aligned16(d.table)) &&
                             et::aligned16(d.delta) && (d.ld_table % 4 == 0) &&
-                            (d.ld_delta % 4 == 0) && et::vec_dim_ok(d.dim) &&
-                            (vec_dim < 0 || vec_dim == d.dim);
+                            (d.ld_delta % 4 == 0) && d.dim % 4 == 0 && d.dim <= 2048 &&
+                            (vec_dim < 0 || vec_dim == cap);
         if (vec_ok) {
-            vec_dim = d.dim;
+            vec_dim = cap;
             pack.vec_mask |= 1u << t;
         } else {
             any_generic = true;

@@ -350,3 +350,36 @@ def test_forward_and_update_capture_in_a_hip_graph(oracle):
     assert torch.equal(out_g, out_e)
     for a, b in zip(graphed, eager):
         assert torch.equal(a.data, b.data)
+
+
+@pytest.mark.parametrize("dim", [20, 40, 96, 200, 1504])
+def test_update_masked_vector_dims(oracle, dim):
+    """Float32 tables of any dim that is a multiple of 4 run the vector SGD kernels at
+    the next power-of-two capacity (masked): exact mode bit-identical to the oracle,
+    chunked mode bit-identical on every column with <= 512 occurrences."""
+    rng = np.random.default_rng(dim)
+    ncols, B, P = 400, 300, 6
+    base = rng.standard_normal((ncols, dim)).astype(np.float32)
+    delta = rng.standard_normal((B, dim)).astype(np.float32)
+    I = rng.integers(1, ncols + 1, (B, P))
+    I[:, :3] = 9  # column 9: 900 occurrences -> chunked partial sums unless exact
+    ref = base.copy()
+    oracle.sgd(ref, delta, I, 0.3, fused=dim * 4 <= 512)
+    for exact in (True, False):
+        A = et.SimpleEmbedding(dev(base), et.Static(dim))
+        et.update_(et.Descent(0.3), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta),
+                                                                dev(I)), exact=exact)
+        got = host(A.data)
+        if exact:
+            assert bits_equal(got, ref)
+        else:
+            keep = np.ones(ncols, bool)
+            keep[8] = False
+            assert bits_equal(got[keep], ref[keep])
+            # the chunked column against the exact fp64 update, at the summation
+            # error-bound scale 1e-6 * (|w| + eta * sum |delta|) (as in the hot-row test)
+            occ = (I == 9).sum(1)
+            exact64 = base[8].astype(np.float64) - np.float64(np.float32(0.3)) * (
+                occ[:, None] * delta.astype(np.float64)).sum(0)
+            scale = np.abs(base[8]) + 0.3 * (occ[:, None] * np.abs(delta)).sum(0)
+            assert np.all(np.abs(got[8] - exact64) <= 1e-6 * scale)
