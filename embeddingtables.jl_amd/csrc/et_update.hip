@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, float* __restrict__ partials, int pdim,
-    uint32_t sent, float eta32, double eta64) {
+    uint32_t sent, float eta32, double eta64, uint32_t my_mask) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
             if (qq + g >= nq || kkey == sent) continue;  // past the end / bad indices
             const int t = table_of_key(pack, ntables, kkey);
             const et_update_desc& d = pack.d[t];
-            if (!((pack.vec_mask >> t) & 1u)) continue;  // the generic kernels' table
+            if (!((my_mask >> t) & 1u)) continue;  // another capacity's / the generic table
             float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
                                       kkey - pack.row_off[t]);
             const int vpr = d.dim / 4;
@@ -418,7 +418,8 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
     const uint32_t* __restrict__ counters, const uint32_t* __restrict__ mlist,
-    const float* __restrict__ partials, int pdim, uint32_t sent, float eta32, double eta64) {
+    const float* __restrict__ partials, int pdim, uint32_t sent, float eta32, double eta64,
+    uint32_t my_mask) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
             const uint32_t seg = mlist[k];
             {
                 const uint32_t key0 = keys[seg_start[seg]];
-                if (key0 == sent || !((pack.vec_mask >> table_of_key(pack, ntables, key0)) & 1u))
+                if (key0 == sent || !((my_mask >> table_of_key(pack, ntables, key0)) & 1u))
                     continue;  // uniform across the workgroup
             }
             const uint32_t p0 = partial_start[seg], np = partial_start[seg + 1] - p0;
@@ -675,10 +676,29 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     return ET_OK;
 }
 
+// Float32 tables on the vector kernels, grouped by power-of-two capacity (one pass of
+// k_sgd_chunks / k_sgd_combine per capacity; each pass skips the other tables).
+struct VecGroups {
+    int n = 0;
+    int cap[8];
+    uint32_t mask[8];
+    bool add(int c, int t) {
+        for (int i = 0; i < n; ++i)
+            if (cap[i] == c) {
+                mask[i] |= 1u << t;
+                return true;
+            }
+        if (n == 8) return false;
+        cap[n] = c;
+        mask[n++] = 1u << t;
+        return true;
+    }
+};
+
 template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
-                     int vec_dim, bool any_generic, hipStream_t s) {
+                     const VecGroups& vg, bool any_generic, hipStream_t s) {
     static const unsigned grid = [] {
         const char* e = getenv("ET_SGD_GRID");  // experiments: workgroups of the SGD passes
         return e ? (unsigned)atoi(e) : 256u * 16u;
@@ -688,12 +708,12 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     case DD:                                                                                   \
         hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
                            ntables, gr.keys, gr.vals, w.recs, w.counters, w.partials, pdim,    \
-                           sent, eta_c, eta64);                                                \
+                           sent, eta_c, eta64, vg.mask[i]);                                    \
         hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,   \
                            ntables, gr.keys, w.seg_start, w.multi, w.counters, w.mlist,        \
-                           w.partials, pdim, sent, eta_c, eta64);                              \
+                           w.partials, pdim, sent, eta_c, eta64, vg.mask[i]);                  \
         break;
-        switch (vec_dim) {
+        for (int i = 0; i < vg.n; ++i) switch (vg.cap[i]) {
             ET_SGD_VEC(16)
             ET_SGD_VEC(32)
             ET_SGD_VEC(64)
@@ -703,7 +723,7 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
             ET_SGD_VEC(1024)
             ET_SGD_VEC(2048)
             default: break;
-        }
+            }
 #undef ET_SGD_VEC
         ET_LAUNCH_CHECK("k_sgd_chunks");
     }
@@ -741,10 +761,10 @@ inline double convert_eta(int dtype, double eta) {
 template <typename T, typename C>
 int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, double eta_c, double eta64,
-                     int mode, bool nt, int vec_dim, bool any_generic, hipStream_t s) {
+                     int mode, bool nt, const VecGroups& vg, bool any_generic, hipStream_t s) {
 #define ET_SGD_CALL(M, NTV)                                                                \
     return launch_sgd_typed<T, C, M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, (C)eta_c, \
-                                          eta64, vec_dim, any_generic, s)
+                                          eta64, vg, any_generic, s)
     if (mode == 0) {
         if (nt) ET_SGD_CALL(0, true);
         ET_SGD_CALL(0, false);
@@ -829,7 +849,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
 
     et::UpdatePack pack;
     uint32_t ro = 0, oo = 0;
-    int vec_dim = -1;
+    et::VecGroups vg;
     bool any_generic = false;
     pack.vec_mask = 0;
     for (int t = 0; t < ntables; ++t) {
@@ -846,9 +866,8 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         const bool vec_ok = dtype == ET_F32 && (d.cols_per_page > 0 || et::aligned16(d.table)) &&
                             et::aligned16(d.delta) && (d.ld_table % 4 == 0) &&
                             (d.ld_delta % 4 == 0) && d.dim % 4 == 0 && d.dim <= 2048 &&
-                            (vec_dim < 0 || vec_dim == cap);
+                            vg.add(cap, t);
         if (vec_ok) {
-            vec_dim = cap;
             pack.vec_mask |= 1u << t;
         } else {
             any_generic = true;
@@ -868,23 +887,23 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     switch (dtype) {
         case ET_F32:
             return et::launch_sgd_dtype<float, float>(pack, ntables, gr, w, chunk, pdim, sent,
-                                                      eta_c, eta, mode, nt, vec_dim,
+                                                      eta_c, eta, mode, nt, vg,
                                                       any_generic, s);
         case ET_F64:
             return et::launch_sgd_dtype<double, double>(pack, ntables, gr, w, chunk, pdim, sent,
-                                                         eta_c, eta, mode, nt, vec_dim,
+                                                         eta_c, eta, mode, nt, vg,
                                                          any_generic, s);
         case ET_BF16:
             return et::launch_sgd_dtype<__bf16, float>(pack, ntables, gr, w, chunk, pdim, sent,
-                                                       eta_c, eta, mode, nt, vec_dim,
+                                                       eta_c, eta, mode, nt, vg,
                                                        any_generic, s);
         default:  // ET_F16
             if (flags & ET_FLAG_F16_FP32_ACC)
                 return et::launch_sgd_dtype<_Float16, float>(pack, ntables, gr, w, chunk, pdim,
-                                                             sent, eta_c, eta, mode, nt, vec_dim,
+                                                             sent, eta_c, eta, mode, nt, vg,
                                                              any_generic, s);
             return et::launch_sgd_dtype<_Float16, _Float16>(pack, ntables, gr, w, chunk, pdim,
-                                                            sent, eta_c, eta, mode, nt, vec_dim,
+                                                            sent, eta_c, eta, mode, nt, vg,
                                                             any_generic, s);
     }
 }
