@@ -34,30 +34,60 @@ __global__ __launch_bounds__(256) void k_fill_index(int64_t* __restrict__ idx, i
     }
 }
 
-// dst[off_r + f, j] = slab_r[f, j] for f < rows_r: one wave per (rank, bag) row segment.
+// dst[off_r + f, j] = slab_r[f, j] for f < rows_r (concat), or the reverse (split):
+// one wave per (rank, bag) row segment.
 struct ConcatPack {
     int32_t rows[64];
     int64_t off[64];
 };
 
-__global__ __launch_bounds__(256) void k_concat_slabs(const char* __restrict__ slabs, int nranks,
-                                                      int64_t slab_ld_b, int64_t batch,
-                                                      ConcatPack pack, char* __restrict__ dst,
-                                                      int64_t ld_dst_b, int es) {
+template <bool SPLIT>
+__global__ __launch_bounds__(256) void k_slab_copy(char* __restrict__ slabs, int nranks,
+                                                   int64_t slab_ld_b, int64_t batch,
+                                                   ConcatPack pack, char* __restrict__ dst,
+                                                   int64_t ld_dst_b, int es) {
     const int64_t w = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     const int r = (int)(w % nranks);
     const int64_t j = w / nranks;
     if (j >= batch) return;
     const int64_t nb = (int64_t)pack.rows[r] * es;
-    const char* src = slabs + ((int64_t)r * batch + j) * slab_ld_b;
-    char* out = dst + j * ld_dst_b + pack.off[r] * es;
+    char* slab = slabs + ((int64_t)r * batch + j) * slab_ld_b;
+    char* mat = dst + j * ld_dst_b + pack.off[r] * es;
+    const char* src = SPLIT ? mat : slab;
+    char* out = SPLIT ? slab : mat;
     if (((uintptr_t)src & 15) == 0 && ((uintptr_t)out & 15) == 0 && (nb & 15) == 0) {
         for (int64_t b = (int64_t)lane * 16; b < nb; b += 64 * 16)
             *reinterpret_cast<u32x4*>(out + b) = *reinterpret_cast<const u32x4*>(src + b);
     } else {
         for (int64_t b = lane; b < nb; b += 64) out[b] = src[b];
     }
+}
+
+template <bool SPLIT>
+int slab_copy(int dtype, void* slabs, int32_t nranks, int64_t slab_ld, int64_t batch,
+              const int32_t* rows, const int64_t* off, void* mat, int64_t ld, void* stream) {
+    const int es = elsize(dtype);
+    if (!es) return fail(ET_ERR_UNSUPPORTED, "dtype %d", dtype);
+    if (nranks <= 0 || nranks > 64) return fail(ET_ERR_ARG, "nranks must be in 1..64");
+    if (batch <= 0) return ET_OK;
+    if (!slabs || !mat || !rows || !off) return fail(ET_ERR_ARG, "NULL argument");
+    ConcatPack pack;
+    for (int r = 0; r < nranks; ++r) {
+        if (rows[r] < 0 || rows[r] > slab_ld) return fail(ET_ERR_ARG, "rank %d rows", r);
+        if (rows[r] > 0 && (off[r] < 0 || off[r] + rows[r] > ld))
+            return fail(ET_ERR_ARG, "rank %d rows outside the matrix", r);
+        pack.rows[r] = rows[r];
+        pack.off[r] = off[r];
+    }
+    const int64_t waves = (int64_t)nranks * batch;
+    const int64_t blocks = (waves + 3) / 4;
+    if (blocks > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+    hipLaunchKernelGGL(k_slab_copy<SPLIT>, dim3((unsigned)blocks), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), static_cast<char*>(slabs), nranks,
+                       slab_ld * es, batch, pack, static_cast<char*>(mat), ld * es, es);
+    ET_LAUNCH_CHECK("k_slab_copy");
+    return ET_OK;
 }
 
 }  // namespace et
@@ -125,27 +155,16 @@ extern "C" int et_concat_slabs(int dtype, const void* slabs, int32_t nranks, int
                                int64_t batch, const int32_t* rows, const int64_t* dst_row_off,
                                void* dst, int64_t ld_dst, void* stream) {
     et::clear_err();
-    const int es = et::elsize(dtype);
-    if (!es) return et::fail(ET_ERR_UNSUPPORTED, "dtype %d", dtype);
-    if (nranks <= 0 || nranks > 64) return et::fail(ET_ERR_ARG, "nranks must be in 1..64");
-    if (batch <= 0) return ET_OK;
-    if (!slabs || !dst || !rows || !dst_row_off) return et::fail(ET_ERR_ARG, "NULL argument");
-    et::ConcatPack pack;
-    for (int r = 0; r < nranks; ++r) {
-        if (rows[r] < 0 || rows[r] > slab_ld) return et::fail(ET_ERR_ARG, "rank %d rows", r);
-        if (rows[r] > 0 && (dst_row_off[r] < 0 || dst_row_off[r] + rows[r] > ld_dst))
-            return et::fail(ET_ERR_ARG, "rank %d rows outside ld_dst", r);
-        pack.rows[r] = rows[r];
-        pack.off[r] = dst_row_off[r];
-    }
-    const int64_t waves = (int64_t)nranks * batch;
-    const int64_t blocks = (waves + 3) / 4;
-    if (blocks > 0x7fffffffll) return et::fail(ET_ERR_ARG, "grid too large");
-    hipLaunchKernelGGL(et::k_concat_slabs, dim3((unsigned)blocks), dim3(256), 0,
-                       static_cast<hipStream_t>(stream), (const char*)slabs, nranks,
-                       slab_ld * es, batch, pack, (char*)dst, ld_dst * es, es);
-    ET_LAUNCH_CHECK("k_concat_slabs");
-    return ET_OK;
+    return et::slab_copy<false>(dtype, const_cast<void*>(slabs), nranks, slab_ld, batch, rows,
+                                dst_row_off, dst, ld_dst, stream);
+}
+
+extern "C" int et_split_slabs(int dtype, const void* src, int64_t ld_src, int64_t batch,
+                              int32_t nranks, const int32_t* rows, const int64_t* src_row_off,
+                              void* slabs, int64_t slab_ld, void* stream) {
+    et::clear_err();
+    return et::slab_copy<true>(dtype, slabs, nranks, slab_ld, batch, rows, src_row_off,
+                               const_cast<void*>(src), ld_src, stream);
 }
 
 extern "C" int et_check_errors(uint64_t* oob_count) {

@@ -45,6 +45,7 @@ EXPORTS = (
     "et_index_build",
     "et_update_indexed",
     "et_concat_slabs",
+    "et_split_slabs",
     "et_fill_uniform",
     "et_fill_index_uniform",
     "et_check_errors",
@@ -118,6 +119,7 @@ def load() -> ctypes.CDLL:
         "et_update_indexed": ([c_int, vp, i64, i64, i64, i32, vp, i64, vp, vp, i64, i64, vp, dbl, u32,
                                vp], c_int),
         "et_concat_slabs": ([c_int, vp, i32, i64, i64, vp, vp, vp, i64, vp], c_int),
+        "et_split_slabs": ([c_int, vp, i64, i64, i32, vp, vp, vp, i64, vp], c_int),
         "et_fill_uniform": ([c_int, vp, i64, u64, u64, dbl, dbl, vp], c_int),
         "et_fill_index_uniform": ([vp, i64, i64, u64, u64, vp], c_int),
         "et_check_errors": ([vp], c_int),

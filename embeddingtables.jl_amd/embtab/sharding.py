@@ -334,6 +334,64 @@ class ShardedMapLookup:
         return dst
 
 
+    # --- backward: the gradients of this rank's pieces --------------------------------
+    def split_rows(self, delta_local: torch.Tensor, send: torch.Tensor):
+        """et_split_slabs: the columns of every rank's pieces out of this rank's batch
+        slice of the gradient, into ``send[rank]`` (the inverse of assemble_chunk)."""
+        L = _lib.load()
+        nb = delta_local.shape[0]
+        for shift, rows, offs in self.launches:
+            rr = (ctypes.c_int32 * self.world)(*rows)
+            oo = (ctypes.c_int64 * self.world)(*offs)
+            base = send.data_ptr() + shift * send.element_size()
+            _lib.check(L.et_split_slabs(
+                _lib.et_dtype(delta_local), delta_local.data_ptr(), _ld(delta_local), nb,
+                self.world, ctypes.addressof(rr), ctypes.addressof(oo), base, self.plan.slab_ld,
+                _lib.stream_handle(delta_local.device)))
+
+    def piece_grads(self, piece_tables, piece_idx, delta: torch.Tensor):
+        """The SparseEmbeddingUpdate of each of this rank's pieces (rrule of the sharded
+        maplookup, src/lookup.jl:374-389 with the intended Slicer advance).
+
+        All-gather layout: ``delta`` is the whole ``(B, k + sum D)`` gradient, present on
+        every rank, and a piece's gradient is a column view of it (no communication).
+        All-to-all layout: ``delta`` is this rank's ``(B_r, k + sum D)`` batch slice; the
+        columns of every rank's pieces are cut out (et_split_slabs) and exchanged with
+        one all-to-all, giving the ``(B, slab)`` gradient of this rank's features.
+        The update itself is then purely local: ``update_(opt, piece_tables, grads, ...)``.
+        """
+        from .update import SparseEmbeddingUpdate
+
+        ps = self.plan.pieces[self.rank]
+        if self.exchange_kind == "allgather":
+            views = [delta[:, p.col:p.col + p.dim] for p in ps]
+        else:
+            import torch.distributed as dist
+
+            ld = self.plan.slab_ld
+            send = torch.zeros((self.world, self.mine, ld), dtype=delta.dtype, device=delta.device)
+            self.split_rows(delta, send)
+            recv = torch.empty((self.batch, ld), dtype=delta.dtype, device=delta.device)
+            sizes_out = [(self.split[j + 1] - self.split[j]) * ld for j in range(self.world)]
+            sizes_in = [self.mine * ld] * self.world
+            if self.world == 1:
+                recv.copy_(send[0])
+            elif self._gloo():
+                host = torch.empty(recv.shape, dtype=recv.dtype)
+                dist.all_to_all_single(host.view(-1), send.cpu().reshape(-1), sizes_out,
+                                       sizes_in, group=self.group)
+                recv.copy_(host)
+            else:
+                dist.all_to_all_single(recv.view(-1), send.view(-1), output_split_sizes=sizes_out,
+                                       input_split_sizes=sizes_in, group=self.group)
+            views, s = [], 0
+            for p in ps:
+                views.append(recv[:, s:s + p.dim])
+                s += p.dim
+        return [SparseEmbeddingUpdate(t.lookup_type, v, i)
+                for t, v, i in zip(piece_tables, views, piece_idx)]
+
+
 class ShardedPreallocation(ShardedMapLookup):
     """Round-1 name: table-wise plan, all-gather exchange, one chunk."""
 

@@ -214,6 +214,14 @@ int et_concat_slabs(int dtype, const void* slabs, int32_t nranks, int64_t slab_l
                     int64_t batch, const int32_t* rows, const int64_t* dst_row_off, void* dst,
                     int64_t ld_dst, void* stream);
 
+/* The reverse of et_concat_slabs, for the backward exchange of a sharded step:
+ * slab_r[:, f] (row f < rows[r] of rank r's (slab_ld x batch) slab, slabs laid out
+ * rank after rank) = src[src_row_off[r] + f, :].  Used to cut a batch-sliced gradient
+ * into per-rank slabs before an all-to-all. */
+int et_split_slabs(int dtype, const void* src, int64_t ld_src, int64_t batch, int32_t nranks,
+                   const int32_t* rows, const int64_t* src_row_off, void* slabs,
+                   int64_t slab_ld, void* stream);
+
 /* Deterministic synthetic data (the same counter-based hash as oracle/):
  * element i of dst = lo + (hi-lo) * u(seed, offset + i), u in [0,1) with 24 bits. */
 int et_fill_uniform(int dtype, void* dst, int64_t n, uint64_t seed, uint64_t offset,

@@ -51,6 +51,12 @@ def test_featurewise_plan_covers_every_feature_once(world):
     assert plan_features([5, 7], 2) == [(0, 5), (5, 12)]  # unsplittable tables
 
 
+class _Tab:
+    """Stand-in piece table for the gradient plumbing (only the lookup type is read)."""
+
+    lookup_type = None
+
+
 def _worker(rank, world, port, sizes, result_q):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
@@ -80,6 +86,12 @@ def _worker(rank, world, port, sizes, result_q):
                     if n:
                         dst[:, o:o + n] = torch.from_numpy(g[r][:, shift:shift + n])
 
+        def split_rows(self, delta_local, send):
+            for shift, rows, offs in self.launches:
+                for r, (n, o) in enumerate(zip(rows, offs)):
+                    if n:
+                        send[r][:, shift:shift + n] = delta_local[:, o:o + n]
+
     plans = {"table": ShardPlan.tablewise(dims, world, k),
              "table_spread": ShardPlan.tablewise(dims, world, k, sizes=sizes),
              "feature": ShardPlan.featurewise(dims, world, k, granule=16)}
@@ -99,6 +111,13 @@ def _worker(rank, world, port, sizes, result_q):
                 sm(ptabs, pidx, dst)
                 lo, hi = sm.split[rank], sm.split[rank + 1]
                 ok = np.array_equal(dst.numpy()[:, k:], ref[lo:hi, k:])
+            # backward: the gradient columns of this rank's pieces, for every bag
+            full = torch.from_numpy(np.random.default_rng(9).standard_normal(
+                (B, plan.ld)).astype(np.float32))
+            local = full if exchange == "allgather" else full[sm.split[rank]:sm.split[rank + 1]]
+            grads = sm.piece_grads([_Tab() for _ in ps], pidx, local.contiguous())
+            for p, g in zip(ps, grads):
+                ok = ok and torch.equal(g.delta, full[:, p.col:p.col + p.dim])
             result_q.put((rank, name, exchange, chunks, bool(ok)))
     dist.destroy_process_group()
 
