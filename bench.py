@@ -458,8 +458,11 @@ def main():
         result["lookup_only_ms"] = kernel_ms
         result["slab_cols"] = plan.slab_ld
         if world > 1 and not args.no_alltoall:
-            result["alltoall"] = bench_alltoall(plan, rank, world, B, device, tables, idx,
-                                                max(5, args.steps // 2), 2)
+            try:  # an extra measurement: never lose the main line to it
+                result["alltoall"] = bench_alltoall(plan, rank, world, B, device, tables, idx,
+                                                    max(5, args.steps // 2), 2)
+            except Exception as e:  # noqa: BLE001
+                result["alltoall"] = {"error": f"{type(e).__name__}: {e}"}
     if world == 1 and not args.no_extra and not sharded:
         # config 3 also at prependrows k = 16 (dst ld = 16 + 3328)
         dst16 = torch.empty((B, 16 + sum(dims)), dtype=torch.float32, device=device)
