@@ -262,7 +262,9 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
             same &= ((d >> b) & 1u) ? ones : ~ones;
         }
         const uint32_t rank = __popcll(same & lt_mask);
-        if (valid && rank == 0) wcnt[wave][d] = (uint32_t)__popcll(same);
+        const bool leader = valid && rank == 0;  // lowest lane of its digit in the wave
+        const uint32_t cnt = (uint32_t)__popcll(same);
+        if (leader) wcnt[wave][d] = cnt;
         __syncthreads();
         uint32_t pos = 0;
         if (valid) {
@@ -270,9 +272,11 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
             for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
         }
         __syncthreads();
-        for (int dd = threadIdx.x; dd < NB; dd += kRsThreads) {
-            base_of[dd] += wcnt[0][dd] + wcnt[1][dd] + wcnt[2][dd] + wcnt[3][dd];
-            wcnt[0][dd] = wcnt[1][dd] = wcnt[2][dd] = wcnt[3][dd] = 0;
+        // only the digits present in this round move: each (wave, digit) leader adds
+        // its count and clears its slot (instead of a pass over all NB digits)
+        if (leader) {
+            atomicAdd(&base_of[d], cnt);
+            wcnt[wave][d] = 0;
         }
         __syncthreads();
         if (valid) {
