@@ -249,11 +249,26 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
     __syncthreads();
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint32_t base = tl * kRsTile;
+    // keys / values of the next round are loaded while this round is ranked
+    uint32_t key_n = 0, val_n = 0;
+    {
+        const uint32_t i = base + threadIdx.x;
+        if (i < n) {
+            key_n = kin[e0 + i];
+            val_n = vin[e0 + i];
+        }
+    }
     for (int r = 0; r < kRsItems; ++r) {
         const uint32_t i = base + r * kRsThreads + threadIdx.x;
         const bool valid = i < n;
-        const uint32_t key = valid ? kin[e0 + i] : 0u;
-        const uint32_t val = valid ? vin[e0 + i] : 0u;
+        const uint32_t key = key_n, val = val_n;
+        if (r + 1 < kRsItems) {
+            const uint32_t i2 = i + kRsThreads;
+            if (i2 < n) {
+                key_n = kin[e0 + i2];
+                val_n = vin[e0 + i2];
+            }
+        }
         const uint32_t d = rs_digit<NB>(key, kb, cap, sh);
         uint64_t same = __ballot(valid);
 #pragma unroll
