@@ -212,10 +212,19 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restri
     const uint32_t n = p.n[k], kb = p.key_base[k], cap = p.key_cap[k], sh = p.shift[k];
     const uint32_t* kp = keys + p.elem0[k];
     const uint32_t base = tl * kRsTile;
-#pragma unroll 4
-    for (int r = 0; r < kRsItems; ++r) {
-        const uint32_t i = base + r * kRsThreads + threadIdx.x;
-        if (i < n) atomicAdd(&h[wave][rs_digit<NB>(kp[i], kb, cap, sh)], 1u);
+    // 8 keys in flight per thread, then their LDS increments
+    for (int r0 = 0; r0 < kRsItems; r0 += 8) {
+        uint32_t kk[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t i = base + (r0 + q) * kRsThreads + threadIdx.x;
+            kk[q] = i < n ? kp[i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t i = base + (r0 + q) * kRsThreads + threadIdx.x;
+            if (i < n) atomicAdd(&h[wave][rs_digit<NB>(kk[q], kb, cap, sh)], 1u);
+        }
     }
     __syncthreads();
     uint32_t* hs = hist + (uint64_t)NB * p.tile_off[k];
