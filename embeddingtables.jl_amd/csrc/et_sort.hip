@@ -81,9 +81,15 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t* __
 
 // Exclusive scan of part[0..np) in place by one workgroup; part[np] = total.
 __global__ __launch_bounds__(kScanThreads) void k_scan_partials(uint32_t* __restrict__ part,
-                                                                int64_t np) {
+                                                                int64_t np,
+                                                                const uint32_t* __restrict__ mlen,
+                                                                uint32_t madd) {
     __shared__ uint32_t lds4[4];
     uint32_t carry = 0;
+    if (mlen) {  // tiles past the device-side length hold zeros and are never read
+        const int64_t used = ((int64_t)*mlen + madd + kScanTile - 1) / kScanTile;
+        np = used < np ? used : np;
+    }
     for (int64_t b0 = 0; b0 < np; b0 += kScanThreads) {
         const int64_t i = b0 + threadIdx.x;
         const uint32_t v = i < np ? part[i] : 0u;
@@ -152,7 +158,7 @@ inline int exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t m, uint
     if (np > 0x7fffffffll) return fail(ET_ERR_ARG, "scan too large");
     hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, m, part,
                        mlen, madd);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, part, np);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, part, np, mlen, madd);
     hipLaunchKernelGGL(k_scan_down, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, out, m,
                        part, mlen, madd);
     ET_LAUNCH_CHECK("exclusive_scan_u32");

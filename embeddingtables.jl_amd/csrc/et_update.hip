@@ -158,17 +158,20 @@ __global__ __launch_bounds__(256) void k_seg_chunks(const uint32_t* __restrict__
                                                     uint32_t chunk, uint32_t* __restrict__ nch,
                                                     uint32_t* __restrict__ multi,
                                                     uint32_t* __restrict__ mlist) {
-    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // grid-stride over entries 0..U only (U is known on the device; the scans below
+    // stop at U + 1), so a fixed grid covers any n
     const uint32_t U = counters[kCntU];
-    if (u > n || u > U) return;  // entries 0..U only: the scans below stop at U + 1
-    uint32_t c = 0;
-    if (u < U) {
-        const uint32_t len = seg_start[u + 1] - seg_start[u];
-        c = len <= chunk ? 1u : (len + chunk - 1) / chunk;
+    for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u <= (int64_t)U && u <= n;
+         u += (int64_t)gridDim.x * 256) {
+        uint32_t c = 0;
+        if (u < U) {
+            const uint32_t len = seg_start[u + 1] - seg_start[u];
+            c = len <= chunk ? 1u : (len + chunk - 1) / chunk;
+        }
+        nch[u] = c;
+        multi[u] = c > 1 ? c : 0u;
+        if (c > 1) mlist[atomicAdd(&counters[kCntM], 1u)] = (uint32_t)u;
     }
-    nch[u] = c;
-    multi[u] = c > 1 ? c : 0u;
-    if (c > 1) mlist[atomicAdd(&counters[kCntM], 1u)] = (uint32_t)u;
 }
 
 // One 16-byte record per chunk — its occurrence range, its column key and where its
@@ -183,20 +186,34 @@ __global__ __launch_bounds__(256) void k_chunk_records(
     const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ seg_start,
     const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ keys,
     uint32_t chunk, uint32_t* __restrict__ counters, ChunkRec* __restrict__ recs) {
-    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    // single-chunk segments: one thread each (grid-stride over the device-side U)
     const uint32_t U = counters[kCntU];
-    if (u == 0) counters[kCntC] = chunk_start[U];
-    if (u >= U) return;
-    const uint32_t ss = seg_start[u], se = seg_start[u + 1], key = keys[ss];
-    const uint32_t cs = chunk_start[u], nc = chunk_start[u + 1] - cs;
-    if (nc == 1) {
-        recs[cs] = ChunkRec{ss, se, key, kApply};
-        return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[kCntC] = chunk_start[U];
+    for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < (int64_t)U;
+         u += (int64_t)gridDim.x * 256) {
+        const uint32_t cs = chunk_start[u];
+        if (chunk_start[u + 1] - cs != 1) continue;  // k_chunk_records_multi's
+        const uint32_t ss = seg_start[u];
+        recs[cs] = ChunkRec{ss, seg_start[u + 1], keys[ss], kApply};
     }
-    const uint32_t ps = partial_start[u];
-    for (uint32_t p = 0; p < nc; ++p) {
-        const uint32_t s0 = ss + p * chunk;
-        recs[cs + p] = ChunkRec{s0, s0 + chunk < se ? s0 + chunk : se, key, ps + p};
+}
+
+// multi-chunk segments (from the appended list): one wave each, lanes over chunks
+__global__ __launch_bounds__(256) void k_chunk_records_multi(
+    const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ seg_start,
+    const uint32_t* __restrict__ partial_start, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ mlist, uint32_t chunk, const uint32_t* __restrict__ counters,
+    ChunkRec* __restrict__ recs) {
+    const uint32_t M = counters[kCntM];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
+        const uint32_t u = mlist[m];
+        const uint32_t ss = seg_start[u], se = seg_start[u + 1], key = keys[ss];
+        const uint32_t cs = chunk_start[u], nc = chunk_start[u + 1] - cs, ps = partial_start[u];
+        for (uint32_t p = lane; p < nc; p += 64) {
+            const uint32_t s0 = ss + p * chunk;
+            recs[cs + p] = ChunkRec{s0, s0 + chunk < se ? s0 + chunk : se, key, ps + p};
+        }
     }
 }
 
@@ -656,13 +673,15 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
         const int64_t np = cdiv64(n, kScanTile);
         hipLaunchKernelGGL(k_seg_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, out.keys,
                            n, w.part);
-        hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, w.part, np);
+        hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, w.part, np,
+                           nullptr, 0u);
         hipLaunchKernelGGL(k_seg_down, dim3((unsigned)np), dim3(kScanThreads), 0, s, out.keys,
                            n, w.part, w.seg_start, w.counters);
         ET_LAUNCH_CHECK("k_seg_down");
     }
     const int64_t blocks1 = cdiv64(n + 1, 256);
-    hipLaunchKernelGGL(k_seg_chunks, dim3((unsigned)blocks1), dim3(256), 0, s, w.seg_start, n,
+    const unsigned fixed_grid = (unsigned)(blocks1 < 8192 ? blocks1 : 8192);
+    hipLaunchKernelGGL(k_seg_chunks, dim3(fixed_grid), dim3(256), 0, s, w.seg_start, n,
                        w.counters, chunk, w.nch, w.multi, w.mlist);
     ET_LAUNCH_CHECK("k_seg_chunks");
     // nch -> chunk_start, multi -> partial_start (in place, n+1 entries)
@@ -670,8 +689,10 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     if (rc != ET_OK) return rc;
     rc = exclusive_scan_u32(w.multi, w.multi, n + 1, w.part, s, w.counters + kCntU, 1);
     if (rc != ET_OK) return rc;
-    hipLaunchKernelGGL(k_chunk_records, dim3((unsigned)blocks), dim3(256), 0, s, w.nch,
-                       w.seg_start, w.multi, out.keys, chunk, w.counters, w.recs);
+    hipLaunchKernelGGL(k_chunk_records, dim3(fixed_grid), dim3(256), 0, s, w.nch, w.seg_start,
+                       w.multi, out.keys, chunk, w.counters, w.recs);
+    hipLaunchKernelGGL(k_chunk_records_multi, dim3(512), dim3(256), 0, s, w.nch, w.seg_start,
+                       w.multi, out.keys, w.mlist, chunk, w.counters, w.recs);
     ET_LAUNCH_CHECK("k_chunk_records");
     return ET_OK;
 }
