@@ -362,7 +362,7 @@ __device__ __forceinline__ void apply_row(float* __restrict__ w,
 // the gradient sum (so the read overlaps the delta gathers) and apply the update;
 // chunks of longer segments store a partial row.
 template <int D, int MODE, bool NT>
-__global__ __launch_bounds__(256, 8) void k_sgd_chunks(
+__global__ __launch_bounds__(256) void k_sgd_chunks(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, float* __restrict__ partials, int pdim,
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(256, 8) void k_sgd_chunks(
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
     constexpr int GPW = 64 / LPR;
-    constexpr int U = NV >= 4 ? 1 : 4 / NV;  // EXPERIMENT
+    constexpr int U = NV >= 8 ? 1 : 8 / NV;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane / LPR, sub = lane % LPR;
     const uint32_t C = counters[kCntC];
