@@ -435,9 +435,12 @@ def main():
             "dim": DIM,
             "table_rows": CRITEO_KAGGLE_ROWS,
             "parallelism": "single GPU" if not sharded else
-                           f"{args.plan} x{world} + "
-                           f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-gather "
-                           f"({shard.chunks} chunks)",
+                           ("table-wise, balanced: contiguous table ranges per GPU, boundary "
+                            "tables cut at 32-feature granularity" if args.plan == "featurewise"
+                            else "table-wise: whole tables per GPU")
+                           + f" x{world} + "
+                           f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-gather concat "
+                           f"({shard.chunks} pipelined batch chunks)",
         },
         "bags_per_s": B * T * args.steps / elapsed,
         "samples_per_s": B * args.steps / elapsed,
