@@ -381,9 +381,21 @@ __device__ __forceinline__ T* col_ptr(const void* table, int64_t ld, int64_t col
 
 // Generic path: any feature size / alignment / per-table dims / paged tables.  One wave
 // per bag, lanes stride over the features, pool order sequential per feature.
-template <typename T, typename A, bool NT>
+// Store conversion T -> O; bfloat16 converts through float (exact for 16-bit types).
+template <typename O, typename T>
+__device__ __forceinline__ O convert_elt(T x) {
+    if constexpr ((__is_same(T, __bf16) || __is_same(O, __bf16)) && !__is_same(T, float) &&
+                  !__is_same(O, float))
+        return O((float)x);
+    else
+        return O(x);
+}
+
+// O: the destination element type (PreallocationStrategy{U}, src/lookup.jl:284-315: the
+// sum is formed in the table's type T, then converted to U on the store).
+template <typename T, typename A, bool NT, typename O = T>
 __global__ __launch_bounds__(256) void k_pooled_generic(LookupPack pack, int ntables,
-                                                        int64_t batch, T* __restrict__ dst,
+                                                        int64_t batch, O* __restrict__ dst,
                                                         int64_t ld_dst) {
     constexpr int K = 4;
     const int64_t item = blockIdx.x;
@@ -395,7 +407,7 @@ __global__ __launch_bounds__(256) void k_pooled_generic(LookupPack pack, int nta
     const int64_t bag = chunk * 4 + wave;
     if (bag >= batch) return;
     const int64_t* ip = d.idx + bag * d.ld_idx;
-    T* out = dst + bag * ld_dst + d.dst_row_off;
+    O* out = dst + bag * ld_dst + d.dst_row_off;
     const int dim = d.dim, pool = d.pool;
     for (int f0 = 0; f0 < dim; f0 += 64 * K) {
         A acc[K];
@@ -419,7 +431,7 @@ __global__ __launch_bounds__(256) void k_pooled_generic(LookupPack pack, int nta
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int f = f0 + lane + 64 * k;
-            if (f < dim) store_scalar<NT>(out + f, T(acc[k]));
+            if (f < dim) store_scalar<NT>(out + f, convert_elt<O>(T(acc[k])));
         }
     }
 }
@@ -713,12 +725,11 @@ int launch_group(int dtype, bool f32acc, GroupKind kind, const LookupPack& pack,
 
 // Validate descriptors, partition them into launch groups and launch.
 // force_gather: every table is a vector (pool == 1) lookup => bit-copy path.
-int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t batch,
-                    void* dst, int64_t ld_dst, uint32_t flags, hipStream_t s) {
-    const int es = elsize(dtype);
-    if (es == 0) return fail(ET_ERR_UNSUPPORTED, "unknown dtype %d", dtype);
+// Descriptor checks shared by the dispatchers (1 = nothing to do).
+int validate_lookup(const et_lookup_desc* descs, int ntables, int64_t batch, const void* dst,
+                    int64_t ld_dst) {
     if (ntables < 0 || batch < 0) return fail(ET_ERR_ARG, "negative ntables/batch");
-    if (ntables == 0 || batch == 0) return ET_OK;
+    if (ntables == 0 || batch == 0) return 1;
     if (!descs) return fail(ET_ERR_ARG, "descs is NULL");
     if (!dst) return fail(ET_ERR_ARG, "dst is NULL");
     for (int t = 0; t < ntables; ++t) {
@@ -738,6 +749,15 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
             if (d.ld_idx < d.pool) return fail(ET_ERR_ARG, "table %d: ld_idx < pool", t);
         }
     }
+    return ET_OK;
+}
+
+int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t batch,
+                    void* dst, int64_t ld_dst, uint32_t flags, hipStream_t s) {
+    const int es = elsize(dtype);
+    if (es == 0) return fail(ET_ERR_UNSUPPORTED, "unknown dtype %d", dtype);
+    const int v = validate_lookup(descs, ntables, batch, dst, ld_dst);
+    if (v != ET_OK) return v == 1 ? ET_OK : v;
     const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
     const bool f32acc = (flags & ET_FLAG_F16_FP32_ACC) != 0;
 
@@ -802,6 +822,63 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
     return ET_OK;
 }
 
+// Tables of one floating type into a destination of another (generic kernel).
+template <typename T, typename A, typename O>
+int launch_convert(const et_lookup_desc* descs, int ntables, int64_t batch, void* dst,
+                   int64_t ld_dst, bool nt, hipStream_t s) {
+    for (int t0 = 0; t0 < ntables; t0 += ET_MAX_TABLES_PER_LAUNCH) {
+        LookupPack pack;
+        int n = 0;
+        for (int t = t0; t < ntables && n < ET_MAX_TABLES_PER_LAUNCH; ++t) pack.d[n++] = descs[t];
+        const int64_t grid = (batch + 3) / 4 * n;
+        if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+        if (nt)
+            hipLaunchKernelGGL((k_pooled_generic<T, A, true, O>), dim3((unsigned)grid), dim3(256),
+                               0, s, pack, n, batch, reinterpret_cast<O*>(dst), ld_dst);
+        else
+            hipLaunchKernelGGL((k_pooled_generic<T, A, false, O>), dim3((unsigned)grid),
+                               dim3(256), 0, s, pack, n, batch, reinterpret_cast<O*>(dst), ld_dst);
+        ET_LAUNCH_CHECK("k_pooled_generic");
+    }
+    return ET_OK;
+}
+
+template <typename T, typename A>
+int convert_to(int out_dtype, const et_lookup_desc* descs, int ntables, int64_t batch, void* dst,
+               int64_t ld_dst, bool nt, hipStream_t s) {
+    switch (out_dtype) {
+        case ET_F32: return launch_convert<T, A, float>(descs, ntables, batch, dst, ld_dst, nt, s);
+        case ET_F64: return launch_convert<T, A, double>(descs, ntables, batch, dst, ld_dst, nt, s);
+        case ET_F16:
+            return launch_convert<T, A, _Float16>(descs, ntables, batch, dst, ld_dst, nt, s);
+        case ET_BF16:
+            return launch_convert<T, A, __bf16>(descs, ntables, batch, dst, ld_dst, nt, s);
+    }
+    return fail(ET_ERR_UNSUPPORTED, "destination dtype %d", out_dtype);
+}
+
+int lookup_dispatch_convert(int dtype, int out_dtype, const et_lookup_desc* descs, int ntables,
+                            int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
+                            hipStream_t s) {
+    const int v = validate_lookup(descs, ntables, batch, dst, ld_dst);
+    if (v != ET_OK) return v == 1 ? ET_OK : v;
+    const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
+    switch (dtype) {
+        case ET_F32: return convert_to<float, float>(out_dtype, descs, ntables, batch, dst, ld_dst, nt, s);
+        case ET_F64:
+            return convert_to<double, double>(out_dtype, descs, ntables, batch, dst, ld_dst, nt, s);
+        case ET_BF16:
+            return convert_to<__bf16, float>(out_dtype, descs, ntables, batch, dst, ld_dst, nt, s);
+        case ET_F16:
+            if (flags & ET_FLAG_F16_FP32_ACC)
+                return convert_to<_Float16, float>(out_dtype, descs, ntables, batch, dst, ld_dst,
+                                                   nt, s);
+            return convert_to<_Float16, _Float16>(out_dtype, descs, ntables, batch, dst, ld_dst,
+                                                  nt, s);
+    }
+    return fail(ET_ERR_UNSUPPORTED, "table dtype %d (conversions are between float types)", dtype);
+}
+
 }  // namespace et
 
 // ---------------------------------------------------------------------------
@@ -860,4 +937,15 @@ extern "C" int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int
     // f16 pool == 1 tables are bit copies; the flag only matters for pool >= 2, where the
     // group kind is kPooledVec / kGeneric.
     return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags, s);
+}
+
+extern "C" int et_maplookup_prealloc_to(int dtype, int dst_dtype, const et_lookup_desc* descs,
+                                        int32_t ntables, int64_t batch, void* dst,
+                                        int64_t ld_dst, uint32_t flags, void* stream) {
+    et::clear_err();
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (dst_dtype == dtype)
+        return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags, s);
+    return et::lookup_dispatch_convert(dtype, dst_dtype, descs, ntables, batch, dst, ld_dst,
+                                       flags, s);
 }

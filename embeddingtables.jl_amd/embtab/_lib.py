@@ -21,7 +21,7 @@ ET_FLAG_EXACT_UPDATE = 4
 ET_FLAG_SGD_UNFUSED = 8
 ET_FLAG_SGD_F64_ALPHA = 16
 ET_MAX_TABLES_PER_LAUNCH = 32
-ET_ABI_VERSION = 2
+ET_ABI_VERSION = 3
 
 TORCH_TO_ET = {
     torch.float32: ET_F32,
@@ -39,6 +39,7 @@ EXPORTS = (
     "et_gather",
     "et_pooled_sum",
     "et_maplookup_prealloc",
+    "et_maplookup_prealloc_to",
     "et_sgd_workspace_size",
     "et_sparse_sgd",
     "et_index_workspace_size",
@@ -112,6 +113,7 @@ def load() -> ctypes.CDLL:
         "et_gather": ([c_int, vp, i64, i64, i32, vp, i64, vp, i64, u32, vp], c_int),
         "et_pooled_sum": ([c_int, vp, i64, i64, i32, vp, i32, i64, i64, vp, i64, u32, vp], c_int),
         "et_maplookup_prealloc": ([c_int, vp, i32, i64, vp, i64, u32, vp], c_int),
+        "et_maplookup_prealloc_to": ([c_int, c_int, vp, i32, i64, vp, i64, u32, vp], c_int),
         "et_sgd_workspace_size": ([vp, i32, vp], c_int),
         "et_sparse_sgd": ([c_int, vp, i32, dbl, u32, vp, i64, vp], c_int),
         "et_index_workspace_size": ([i64, vp], c_int),

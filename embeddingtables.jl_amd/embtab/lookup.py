@@ -221,7 +221,7 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
         raise ArgumentError("destination features must be contiguous")
     if k + sum(featuresize(t) for t in tables) > dst.shape[1]:
         raise ArgumentError("destination has too few rows for prependrows + sum(D)")
-    dtype = dst.dtype
+    dtype = tables[0].dtype  # the tables' element type; dst may be another (U)
     descs = (_lib.LookupDesc * len(tables))()
     off = k
     for t, (A, i) in enumerate(zip(tables, Is)):
@@ -229,8 +229,8 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
         _check_idx(i)
         if A.dtype != dtype:
             raise NotImplementedError(
-                f"table {t} eltype {A.dtype} != destination eltype {dtype} "
-                "(PreallocationStrategy{T} conversion is not implemented on the GPU)")
+                f"table {t} eltype {A.dtype} != table 0 eltype {dtype}: one launch takes "
+                "tables of one element type")
         if _trailing_size(i) != B:
             raise ArgumentError(f"table {t}: batch {_trailing_size(i)} != {B}")
         D, R = A.size()
@@ -240,7 +240,12 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
                                    1 if i.dim() == 1 else _ld(i), off, cpp)
         off += D
     flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
-    _lib.check(_lib.load().et_maplookup_prealloc(
-        _lib.et_dtype(dst), ctypes.addressof(descs), len(tables), B, dst.data_ptr(), _ld(dst),
-        flags, _lib.stream_handle(dst.device)))
+    if dst.dtype == dtype:
+        _lib.check(_lib.load().et_maplookup_prealloc(
+            _lib.et_dtype(dst), ctypes.addressof(descs), len(tables), B, dst.data_ptr(),
+            _ld(dst), flags, _lib.stream_handle(dst.device)))
+    else:  # PreallocationStrategy{U}: sums in the table type, converted on the store
+        _lib.check(_lib.load().et_maplookup_prealloc_to(
+            _lib.TORCH_TO_ET[dtype], _lib.et_dtype(dst), ctypes.addressof(descs), len(tables),
+            B, dst.data_ptr(), _ld(dst), flags, _lib.stream_handle(dst.device)))
     return dst

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 2
+#define ET_ABI_VERSION 3
 
 /* Status codes. */
 #define ET_OK 0
@@ -130,6 +130,15 @@ typedef struct et_lookup_desc {
 int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int32_t ntables,
                           int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                           void* stream);
+
+/* PreallocationStrategy{U} with a destination of another floating type than the
+ * tables (src/lookup.jl:284-315: `similar(example(x), U, ...)`): every pooled sum is
+ * formed in the table type (dtype; ET_FLAG_F16_FP32_ACC as for et_pooled_sum), then
+ * converted to dst_dtype on the store.  Float types only (ET_F32/F64/F16/BF16);
+ * dst_dtype == dtype is et_maplookup_prealloc. */
+int et_maplookup_prealloc_to(int dtype, int dst_dtype, const et_lookup_desc* descs,
+                             int32_t ntables, int64_t batch, void* dst, int64_t ld_dst,
+                             uint32_t flags, void* stream);
 
 /* One table of a (multi-table) fused sparse-SGD update. */
 typedef struct et_update_desc {

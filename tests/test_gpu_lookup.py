@@ -448,3 +448,36 @@ def test_sharded_training_step_simulated_ranks(oracle, exact):
         et.update_(et.Descent(0.1), ptabs, grads, [et.Indexer() for _ in ptabs], exact=exact)
     for a, b in zip(full, ref):
         assert torch.equal(a.data, b.data)
+
+
+@pytest.mark.parametrize("src,dst", [("f16", torch.float32), ("f32", torch.float16),
+                                     ("bf16", torch.float32), ("f32", torch.bfloat16),
+                                     ("f64", torch.float32)])
+def test_preallocation_eltype_conversion(oracle, src, dst):
+    """PreallocationStrategy{U} (src/lookup.jl:284-315): sums in the table type, then
+    one conversion to the destination type U on the store."""
+    rng = np.random.default_rng(17)
+    dims, rows, B, P, k = [64, 40, 128], [300, 50, 1000], 200, 12, 3
+    raw = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
+    if src == "bf16":
+        hs = [oracle.f32_to_bf16(x) for x in raw]
+        tabs = [et.SimpleEmbedding(dev(h).view(torch.bfloat16)) for h in hs]
+    else:
+        npt = {"f16": np.float16, "f32": np.float32, "f64": np.float64}[src]
+        hs = [x.astype(npt) for x in raw]
+        tabs = [et.SimpleEmbedding(dev(h)) for h in hs]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    out = et.maplookup(et.PreallocationStrategy(k, eltype=dst), tabs, [dev(i) for i in hidx])
+    assert out.dtype == dst and out.shape == (B, k + sum(dims))
+    ref_t = oracle.maplookup_prealloc(hs, hidx, prependrows=k, bf16=src == "bf16")[:, k:]
+    as32 = oracle.bf16_to_f32(ref_t) if src == "bf16" else ref_t.astype(np.float64)
+    if dst == torch.float32:
+        ref = np.asarray(as32, np.float32)
+        got = host(out[:, k:])
+    elif dst == torch.float16:
+        ref = np.asarray(as32, np.float32).astype(np.float16).view(np.uint16)
+        got = host(out[:, k:].view(torch.int16)).view(np.uint16)
+    else:
+        ref = oracle.f32_to_bf16(np.asarray(as32, np.float32))
+        got = host(out[:, k:].view(torch.int16)).view(np.uint16)
+    assert bits_equal(got, ref)
