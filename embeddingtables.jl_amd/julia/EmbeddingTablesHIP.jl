@@ -208,8 +208,10 @@ function lookup!(dst, A::HipSplitEmbedding{S,T}, I::Union{HipVector{Int},HipMatr
     return dst
 end
 
-function maplookup!(strategy::PreallocationStrategy, dst::HipMatrix{T},
-                    x::Vector{<:HipTable{<:Any,T}}, I0; kw...) where {T}
+# dst may have another float eltype U than the tables (PreallocationStrategy{U},
+# src/lookup.jl:284-315): then the _to entry converts on the store.
+function maplookup!(strategy::PreallocationStrategy, dst::HipMatrix{U},
+                    x::Vector{<:HipTable{<:Any,T}}, I0; kw...) where {U,T}
     I = EmbeddingTables.colwrap(I0)
     descs = Vector{LookupDesc}(undef, length(x))
     off = strategy.prependrows
@@ -219,10 +221,11 @@ function maplookup!(strategy::PreallocationStrategy, dst::HipMatrix{T},
         descs[t] = LookupDesc(tp, ldt, size(A, 2), size(A, 1), pool, pointer(i), pool, off, cpp)
         off += size(A, 1)
     end
-    check(ccall((:et_maplookup_prealloc, libembtab), Cint,
-                (Cint, Ptr{LookupDesc}, Int32, Int64, Ptr{Cvoid}, Int64, UInt32, Ptr{Cvoid}),
-                et_dtype(T), descs, length(descs), EmbeddingTables._batchsize(I), dst.ptr,
-                leading(dst), ET_FLAG_NONTEMPORAL, stream()))
+    check(ccall((:et_maplookup_prealloc_to, libembtab), Cint,
+                (Cint, Cint, Ptr{LookupDesc}, Int32, Int64, Ptr{Cvoid}, Int64, UInt32,
+                 Ptr{Cvoid}),
+                et_dtype(T), et_dtype(U), descs, length(descs), EmbeddingTables._batchsize(I),
+                dst.ptr, leading(dst), ET_FLAG_NONTEMPORAL, stream()))
     return dst
 end
 
