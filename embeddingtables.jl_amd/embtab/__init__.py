@@ -12,7 +12,7 @@ from .tables import (AbstractEmbeddingTable, AbstractLookupType, ArgumentError, 
                      Forward, IndexingContext, NoContext, SimpleEmbedding, SplitEmbedding, Static,
                      Update, columnpointer, example, featuresize)
 from .lookup import (AbstractExecutionStrategy, DefaultStrategy, NoTangent,
-                     PreallocationStrategy, SimpleParallelStrategy, colwrap, destination, lookup,
+                     PreallocationPlan, PreallocationStrategy, SimpleParallelStrategy, colwrap, destination, lookup,
                      lookup_, maplookup, maplookup_)
 from .update import (AbstractIndexer, DenseIndexer, Descent, Indexer, IndexerView,
                      SparseEmbeddingUpdate, SparseIndexer, ensemble_update, gettranslations,
@@ -24,7 +24,7 @@ __all__ = [
     "AbstractEmbeddingTable", "AbstractLookupType", "ArgumentError", "Dynamic", "Static",
     "IndexingContext", "NoContext", "Forward", "Update", "SimpleEmbedding", "SplitEmbedding",
     "featuresize", "example", "columnpointer", "AbstractExecutionStrategy", "DefaultStrategy",
-    "SimpleParallelStrategy", "PreallocationStrategy", "NoTangent", "colwrap", "destination",
+    "SimpleParallelStrategy", "PreallocationStrategy", "PreallocationPlan", "NoTangent", "colwrap", "destination",
     "lookup", "lookup_", "maplookup", "maplookup_", "SparseEmbeddingUpdate", "uncompress",
     "rrule", "Descent", "AbstractIndexer", "Indexer", "SparseIndexer", "DenseIndexer",
     "IndexerView", "index_", "gettranslations", "update_", "optimise_update_",

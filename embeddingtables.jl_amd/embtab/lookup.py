@@ -213,39 +213,69 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
 
     if not tables:
         return dst
-    B = _batchsize(Is)
-    k = strategy.prependrows
-    if dst.dim() != 2 or dst.shape[0] != B:
-        raise ArgumentError(f"destination must be ({B}, prependrows + sum(D))")
-    if dst.numel() > 0 and dst.stride(1) != 1:
-        raise ArgumentError("destination features must be contiguous")
-    if k + sum(featuresize(t) for t in tables) > dst.shape[1]:
-        raise ArgumentError("destination has too few rows for prependrows + sum(D)")
-    dtype = tables[0].dtype  # the tables' element type; dst may be another (U)
-    descs = (_lib.LookupDesc * len(tables))()
-    off = k
-    for t, (A, i) in enumerate(zip(tables, Is)):
-        _check_table(A)
-        _check_idx(i)
-        if A.dtype != dtype:
-            raise NotImplementedError(
-                f"table {t} eltype {A.dtype} != table 0 eltype {dtype}: one launch takes "
-                "tables of one element type")
-        if _trailing_size(i) != B:
-            raise ArgumentError(f"table {t}: batch {_trailing_size(i)} != {B}")
-        D, R = A.size()
-        pool = 1 if i.dim() == 1 else int(i.shape[1])
-        table, cpp = A.device_table()
-        descs[t] = _lib.LookupDesc(table, A.ld, R, D, pool, i.data_ptr(),
-                                   1 if i.dim() == 1 else _ld(i), off, cpp)
-        off += D
-    flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
-    if dst.dtype == dtype:
-        _lib.check(_lib.load().et_maplookup_prealloc(
-            _lib.et_dtype(dst), ctypes.addressof(descs), len(tables), B, dst.data_ptr(),
-            _ld(dst), flags, _lib.stream_handle(dst.device)))
-    else:  # PreallocationStrategy{U}: sums in the table type, converted on the store
-        _lib.check(_lib.load().et_maplookup_prealloc_to(
-            _lib.TORCH_TO_ET[dtype], _lib.et_dtype(dst), ctypes.addressof(descs), len(tables),
-            B, dst.data_ptr(), _ld(dst), flags, _lib.stream_handle(dst.device)))
-    return dst
+    return PreallocationPlan(strategy, dst, tables, Is, nontemporal)()
+
+
+class PreallocationPlan:
+    """``maplookup!(PreallocationStrategy(k), dst, tables, I)`` with the descriptors
+    validated and built once for fixed tables, index buffers and destination: each
+    call is one call into the library (no per-table Python work) — for serving loops
+    that refill the index buffers in place, and for the sharded step's chunks."""
+
+    def __init__(self, strategy: PreallocationStrategy, dst, tables, I, nontemporal=True):
+        tables = list(tables)
+        Is = colwrap(I)
+        if len(Is) != len(tables):
+            raise ArgumentError(f"{len(tables)} tables but {len(Is)} index arrays")
+        if not tables:
+            raise ArgumentError("a plan needs at least one table")
+        B = _batchsize(Is)
+        k = strategy.prependrows
+        if dst.dim() != 2 or dst.shape[0] != B:
+            raise ArgumentError(f"destination must be ({B}, prependrows + sum(D))")
+        if dst.numel() > 0 and dst.stride(1) != 1:
+            raise ArgumentError("destination features must be contiguous")
+        if k + sum(featuresize(t) for t in tables) > dst.shape[1]:
+            raise ArgumentError("destination has too few rows for prependrows + sum(D)")
+        dtype = tables[0].dtype  # the tables' element type; dst may be another (U)
+        descs = (_lib.LookupDesc * len(tables))()
+        off = k
+        for t, (A, i) in enumerate(zip(tables, Is)):
+            _check_table(A)
+            _check_idx(i)
+            if A.dtype != dtype:
+                raise NotImplementedError(
+                    f"table {t} eltype {A.dtype} != table 0 eltype {dtype}: one launch takes "
+                    "tables of one element type")
+            if _trailing_size(i) != B:
+                raise ArgumentError(f"table {t}: batch {_trailing_size(i)} != {B}")
+            D, R = A.size()
+            pool = 1 if i.dim() == 1 else int(i.shape[1])
+            table, cpp = A.device_table()
+            descs[t] = _lib.LookupDesc(table, A.ld, R, D, pool, i.data_ptr(),
+                                       1 if i.dim() == 1 else _ld(i), off, cpp)
+            off += D
+        self._keep = (dst, tables, Is)  # the buffers the descriptors point into
+        self._descs = descs
+        self._n = len(tables)
+        self._B = B
+        self._flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
+        self._src = _lib.TORCH_TO_ET[dtype]
+        self._dst_t = _lib.et_dtype(dst)
+        self._dst = dst
+        self._ld = _ld(dst)
+        self._lib = _lib.load()
+
+    def __call__(self):
+        """Launch on the current stream; returns the destination."""
+        dst = self._dst
+        stream = _lib.stream_handle(dst.device)
+        if self._src == self._dst_t:
+            _lib.check(self._lib.et_maplookup_prealloc(
+                self._src, ctypes.addressof(self._descs), self._n, self._B, dst.data_ptr(),
+                self._ld, self._flags, stream))
+        else:  # PreallocationStrategy{U}: sums in the table type, converted on the store
+            _lib.check(self._lib.et_maplookup_prealloc_to(
+                self._src, self._dst_t, ctypes.addressof(self._descs), self._n, self._B,
+                dst.data_ptr(), self._ld, self._flags, stream))
+        return dst

@@ -227,6 +227,7 @@ class ShardedMapLookup:
         self.chunks = max(1, min(chunks, batch)) if exchange == "allgather" else 1
         ld = plan.slab_ld
         self.slab = torch.zeros((batch, ld), dtype=dtype, device=device)
+        self._plans = {}  # lookup_chunk descriptor cache
         # chunk c covers batch rows [bounds[c], bounds[c+1])
         self.bounds = [batch * c // self.chunks for c in range(self.chunks + 1)]
         if exchange == "allgather":
@@ -246,11 +247,22 @@ class ShardedMapLookup:
     # --- device work (overridable so that the CPU rehearsal can stand in the oracle) ---
     def lookup_chunk(self, piece_tables, piece_idx, b0: int, b1: int):
         """One fused launch per width group: this rank's pieces, bags [b0, b1) -> slab."""
-        from .lookup import PreallocationStrategy, maplookup_
+        from .lookup import PreallocationPlan, PreallocationStrategy
 
-        if piece_tables:
-            maplookup_(PreallocationStrategy(0), self.slab[b0:b1], piece_tables,
-                       [i[b0:b1] for i in piece_idx])
+        if not piece_tables:
+            return
+        # descriptor arrays cached per (chunk, tables, index buffers): a training loop
+        # that refills the same index buffers pays one library call per chunk
+        key = (b0, b1, tuple((id(t), t.device_table()) for t in piece_tables),
+               tuple((i.data_ptr(), tuple(i.shape), tuple(i.stride())) for i in piece_idx))
+        plan = self._plans.get(key)
+        if plan is None:
+            if len(self._plans) >= 64:
+                self._plans.clear()
+            plan = PreallocationPlan(PreallocationStrategy(0), self.slab[b0:b1], piece_tables,
+                                     [i[b0:b1] for i in piece_idx])
+            self._plans[key] = plan
+        plan()
 
     def assemble_chunk(self, gathered: torch.Tensor, dst: torch.Tensor):
         """et_concat_slabs: every rank's slab columns into their destination columns."""

@@ -481,3 +481,45 @@ def test_preallocation_eltype_conversion(oracle, src, dst):
         ref = oracle.f32_to_bf16(np.asarray(as32, np.float32))
         got = host(out[:, k:].view(torch.int16)).view(np.uint16)
     assert bits_equal(got, ref)
+
+
+def test_preallocation_plan_reuse(oracle):
+    """PreallocationPlan: descriptors built once; refilling the index buffers in place
+    and calling again gives the new result (same kernels as maplookup!)."""
+    rng = np.random.default_rng(23)
+    dims, rows, B, P, k = [128, 64, 40, 128], [5000, 300, 77, 1000], 256, 20, 2
+    hs = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
+    tabs = [et.SimpleEmbedding(dev(h), et.Static(h.shape[1])) for h in hs]
+    tabs[3] = et.SplitEmbedding(dev(hs[3]), 100)
+    idx = [dev(rng.integers(1, r + 1, (B, P))) for r in rows]
+    dst = torch.zeros((B, k + sum(dims)), dtype=torch.float32, device=DEV)
+    plan = et.PreallocationPlan(et.PreallocationStrategy(k), dst, tabs, idx)
+    for it in range(3):
+        hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+        for d, h in zip(idx, hidx):
+            d.copy_(torch.from_numpy(h))
+        assert plan() is dst
+        ref = oracle.maplookup_prealloc(hs, hidx, prependrows=k)
+        assert bits_equal(host(dst[:, k:]), ref[:, k:])
+    # graph-captured plan replay sees refilled indices too
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        plan()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        plan()
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    for d, h in zip(idx, hidx):
+        d.copy_(torch.from_numpy(h))
+    g.replay()
+    torch.cuda.synchronize()
+    assert bits_equal(host(dst[:, k:]), oracle.maplookup_prealloc(hs, hidx, prependrows=k)[:, k:])
+    # a half-precision destination through the same plan type
+    dst16 = torch.zeros((B, k + sum(dims)), dtype=torch.float16, device=DEV)
+    et.PreallocationPlan(et.PreallocationStrategy(k), dst16, tabs, idx)()
+    ref16 = oracle.maplookup_prealloc(hs, hidx, prependrows=k)[:, k:].astype(np.float16)
+    assert bits_equal(host(dst16[:, k:]), ref16)
+    with pytest.raises(et.ArgumentError):
+        et.PreallocationPlan(et.PreallocationStrategy(k), dst[:, :100], tabs, idx)
