@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="N > 1 process group: nccl (= RCCL on ROCm) or gloo (rehearsal of "
                         "the N > 1 path with several ranks sharing one GPU)")
+    p.add_argument("--p2p", action="store_true",
+                   help="N>1: also time the one-sided exchange (IPC-mapped peers, et_push_cols)")
     p.add_argument("--no-alltoall", action="store_true",
                    help="N > 1: skip the extra all-to-all (batch-sliced output) measurement")
     p.add_argument("--subset", choices=["all", "heavy", "light"], default="all",
@@ -227,6 +229,39 @@ def bench_alltoall(plan, rank, world, B, device, tables, idx, steps, warmup):
     ms = 1e3 * float(el.item()) / steps
     return {"ms_per_step": ms, "value": B * len(plan.dims) * POOL / (ms * 1e-3),
             "unit": "lookups/s", "output": "batch slice per rank"}
+
+
+def bench_p2p(plan, rank, world, B, device, tables, idx, steps, warmup, chunks):
+    """One-sided exchange (fused P2P writes): lookups straight
+    into this rank's columns of its destination, et_push_cols stores them into every
+    peer's IPC-mapped destination, a one-element all-reduce publishes them."""
+    import torch
+    import torch.distributed as dist
+    from embtab.sharding import ShardedMapLookup
+
+    sm = ShardedMapLookup(plan, rank, world, B, torch.float32, device, exchange="p2p",
+                          chunks=chunks)
+    try:
+        for _ in range(warmup):
+            sm(tables, idx, None)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sm(tables, idx, None)
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        sm.close()
+    ms = 1e3 * float(el.item()) / steps
+    return {"ms_per_step": ms, "value": B * len(plan.dims) * POOL / (ms * 1e-3),
+            "unit": "lookups/s", "output": "whole destination on every rank",
+            "chunks": sm.chunks}
 
 
 def zipf_indices(R, shape, alpha, gen, device):
@@ -466,6 +501,12 @@ def main():
                                                     max(5, args.steps // 2), 2)
             except Exception as e:  # noqa: BLE001
                 result["alltoall"] = {"error": f"{type(e).__name__}: {e}"}
+        if world > 1 and args.p2p:
+            try:
+                result["p2p"] = bench_p2p(plan, rank, world, B, device, tables, idx,
+                                          max(5, args.steps // 2), 2, args.chunks)
+            except Exception as e:  # noqa: BLE001
+                result["p2p"] = {"error": f"{type(e).__name__}: {e}"}
     if world == 1 and not args.no_extra and not sharded:
         # config 3 also at prependrows k = 16 (dst ld = 16 + 3328)
         dst16 = torch.empty((B, 16 + sum(dims)), dtype=torch.float32, device=device)

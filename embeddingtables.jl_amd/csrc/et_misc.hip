@@ -90,7 +90,104 @@ int slab_copy(int dtype, void* slabs, int32_t nranks, int64_t slab_ld, int64_t b
     return ET_OK;
 }
 
+// One-sided exchange of a sharded step ("fused P2P xGMI
+// writes"): every 16-byte vector of this rank's destination columns is read once
+// and stored straight into the same columns of each peer's destination (mapped
+// with et_ipc_open).  One thread per vector; the system-scope fence makes the
+// remote stores visible before the kernel retires, so a stream-ordered barrier
+// after the launch (a one-element RCCL all-reduce) publishes them.
+struct PeerPack {
+    char* p[ET_MAX_PEERS];
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_push_cols(const char* __restrict__ src, int64_t ld_b,
+                                                   int64_t batch, int64_t nb, PeerPack peers,
+                                                   int npeers) {
+    const int64_t per_row = VEC ? nb >> 4 : nb;
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < batch * per_row) {
+        const int64_t j = t / per_row;
+        const int64_t o = j * ld_b + (t - j * per_row) * (VEC ? 16 : 1);
+        if constexpr (VEC) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(src + o);
+            for (int q = 0; q < npeers; ++q) *reinterpret_cast<u32x4*>(peers.p[q] + o) = v;
+        } else {
+            const char v = src[o];
+            for (int q = 0; q < npeers; ++q) peers.p[q][o] = v;
+        }
+    }
+    __threadfence_system();
+}
+
 }  // namespace et
+
+extern "C" int et_push_cols(int dtype, const void* src, int64_t ld, int64_t batch, int64_t col,
+                            int64_t ncols, void* const* peers, int32_t npeers, void* stream) {
+    et::clear_err();
+    const int es = et::elsize(dtype);
+    if (!es) return et::fail(ET_ERR_UNSUPPORTED, "dtype %d", dtype);
+    if (npeers < 0 || npeers > ET_MAX_PEERS)
+        return et::fail(ET_ERR_ARG, "npeers must be in 0..%d", ET_MAX_PEERS);
+    if (batch < 0 || ncols < 0 || col < 0 || col + ncols > ld)
+        return et::fail(ET_ERR_ARG, "columns [%lld, %lld) outside ld %lld", (long long)col,
+                        (long long)(col + ncols), (long long)ld);
+    if (batch == 0 || ncols == 0 || npeers == 0) return ET_OK;
+    if (!src || !peers) return et::fail(ET_ERR_ARG, "NULL argument");
+    et::PeerPack pack = {};
+    bool vec = ((uintptr_t)src & 15) == 0 && ((ld * es) & 15) == 0 && ((col * es) & 15) == 0 &&
+               ((ncols * es) & 15) == 0;
+    for (int q = 0; q < npeers; ++q) {
+        if (!peers[q]) return et::fail(ET_ERR_ARG, "peer %d is NULL", q);
+        pack.p[q] = static_cast<char*>(peers[q]) + col * es;
+        vec = vec && ((uintptr_t)peers[q] & 15) == 0;
+    }
+    const char* s = static_cast<const char*>(src) + col * es;
+    const int64_t nb = ncols * es;
+    const int64_t threads = batch * (vec ? nb / 16 : nb);
+    const int64_t blocks = (threads + 255) / 256;
+    if (blocks > 0x7fffffffll) return et::fail(ET_ERR_ARG, "grid too large");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (vec)
+        hipLaunchKernelGGL(et::k_push_cols<true>, dim3((unsigned)blocks), dim3(256), 0, st, s,
+                           ld * es, batch, nb, pack, npeers);
+    else
+        hipLaunchKernelGGL(et::k_push_cols<false>, dim3((unsigned)blocks), dim3(256), 0, st, s,
+                           ld * es, batch, nb, pack, npeers);
+    ET_LAUNCH_CHECK("k_push_cols");
+    return ET_OK;
+}
+
+extern "C" int et_ipc_handle(const void* ptr, void* handle, int64_t* offset) {
+    et::clear_err();
+    if (!ptr || !handle || !offset) return et::fail(ET_ERR_ARG, "NULL argument");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    ET_HIP_CHECK(hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)));
+    hipIpcMemHandle_t h;
+    ET_HIP_CHECK(hipIpcGetMemHandle(&h, base));
+    memcpy(handle, &h, sizeof(h));
+    *offset = static_cast<const char*>(ptr) - static_cast<const char*>(base);
+    return ET_OK;
+}
+
+extern "C" int et_ipc_open(const void* handle, int64_t offset, void** ptr) {
+    et::clear_err();
+    if (!handle || !ptr || offset < 0) return et::fail(ET_ERR_ARG, "bad argument");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    void* base = nullptr;
+    ET_HIP_CHECK(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess));
+    *ptr = static_cast<char*>(base) + offset;
+    return ET_OK;
+}
+
+extern "C" int et_ipc_close(void* ptr, int64_t offset) {
+    et::clear_err();
+    if (!ptr || offset < 0) return et::fail(ET_ERR_ARG, "bad argument");
+    ET_HIP_CHECK(hipIpcCloseMemHandle(static_cast<char*>(ptr) - offset));
+    return ET_OK;
+}
 
 extern "C" int et_abi_version(void) { return ET_ABI_VERSION; }
 

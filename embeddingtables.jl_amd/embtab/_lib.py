@@ -21,7 +21,8 @@ ET_FLAG_EXACT_UPDATE = 4
 ET_FLAG_SGD_UNFUSED = 8
 ET_FLAG_SGD_F64_ALPHA = 16
 ET_MAX_TABLES_PER_LAUNCH = 32
-ET_ABI_VERSION = 3
+ET_ABI_VERSION = 4
+ET_MAX_PEERS = 16
 
 TORCH_TO_ET = {
     torch.float32: ET_F32,
@@ -47,6 +48,10 @@ EXPORTS = (
     "et_update_indexed",
     "et_concat_slabs",
     "et_split_slabs",
+    "et_push_cols",
+    "et_ipc_handle",
+    "et_ipc_open",
+    "et_ipc_close",
     "et_fill_uniform",
     "et_fill_index_uniform",
     "et_check_errors",
@@ -122,6 +127,10 @@ def load() -> ctypes.CDLL:
                                vp], c_int),
         "et_concat_slabs": ([c_int, vp, i32, i64, i64, vp, vp, vp, i64, vp], c_int),
         "et_split_slabs": ([c_int, vp, i64, i64, i32, vp, vp, vp, i64, vp], c_int),
+        "et_push_cols": ([c_int, vp, i64, i64, i64, i64, vp, i32, vp], c_int),
+        "et_ipc_handle": ([vp, vp, vp], c_int),
+        "et_ipc_open": ([vp, i64, vp], c_int),
+        "et_ipc_close": ([vp, i64], c_int),
         "et_fill_uniform": ([c_int, vp, i64, u64, u64, dbl, dbl, vp], c_int),
         "et_fill_index_uniform": ([vp, i64, i64, u64, u64, vp], c_int),
         "et_check_errors": ([vp], c_int),

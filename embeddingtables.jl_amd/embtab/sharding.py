@@ -220,13 +220,14 @@ class ShardedMapLookup:
                  group=None, exchange: str = "allgather", chunks: int = 1):
         if plan.world != world:
             raise ValueError("plan and world size differ")
-        if exchange not in ("allgather", "alltoall"):
+        if exchange not in ("allgather", "alltoall", "p2p"):
             raise ValueError(f"unknown exchange {exchange!r}")
         self.plan, self.rank, self.world, self.batch = plan, rank, world, batch
         self.device, self.group, self.exchange_kind = torch.device(device), group, exchange
-        self.chunks = max(1, min(chunks, batch)) if exchange == "allgather" else 1
+        self.chunks = max(1, min(chunks, batch)) if exchange != "alltoall" else 1
         ld = plan.slab_ld
-        self.slab = torch.zeros((batch, ld), dtype=dtype, device=device)
+        self.slab = (torch.zeros((batch, ld), dtype=dtype, device=device)
+                     if exchange != "p2p" else None)
         self._plans = {}  # lookup_chunk descriptor cache
         # chunk c covers batch rows [bounds[c], bounds[c+1])
         self.bounds = [batch * c // self.chunks for c in range(self.chunks + 1)]
@@ -234,6 +235,14 @@ class ShardedMapLookup:
             self.gathered = [torch.empty((world, self.bounds[c + 1] - self.bounds[c], ld),
                                          dtype=dtype, device=device)
                              for c in range(self.chunks)]
+        elif exchange == "p2p":
+            # every rank's whole destination, mapped into every other rank (et_ipc_open);
+            # this rank's lookups write its own columns in place and et_push_cols stores
+            # them into the peers' copies: no slab, no gathered buffer, no assembly
+            self.out = torch.zeros((batch, plan.ld), dtype=dtype, device=device)
+            self._peers, self._peer_offs = self._open_peers()
+            self._flag = torch.zeros(1, dtype=torch.int32, device=device)
+            self._groups = self._run_groups()
         else:
             # rank j receives batch rows [split[j], split[j+1]) from every rank
             self.split = [batch * j // world for j in range(world + 1)]
@@ -241,7 +250,7 @@ class ShardedMapLookup:
             self.gathered = [torch.empty((world, self.mine, ld), dtype=dtype, device=device)]
         self.launches = plan.assembly_launches()
         self._comm = (torch.cuda.Stream(self.device) if self.device.type == "cuda"
-                      and self.chunks > 1 else None)
+                      and (self.chunks > 1 or exchange == "p2p") else None)
         self._events = []
 
     # --- device work (overridable so that the CPU rehearsal can stand in the oracle) ---
@@ -276,6 +285,117 @@ class ShardedMapLookup:
                 _lib.et_dtype(dst), base, self.world, self.plan.slab_ld, nb,
                 ctypes.addressof(rr), ctypes.addressof(oo), dst.data_ptr(), _ld(dst),
                 _lib.stream_handle(dst.device)))
+
+    # --- one-sided exchange (exchange="p2p") --------------------------------------------
+    def _run_groups(self):
+        """``(dst_col, ncols, [piece positions])`` per contiguous run of this rank's pieces."""
+        groups, pos = [], 0
+        for _, dcol, n in self.plan.runs(self.rank):
+            members, width = [], 0
+            while width < n:
+                members.append(pos)
+                width += self.plan.pieces[self.rank][pos].dim
+                pos += 1
+            groups.append((dcol, n, members))
+        return groups
+
+    def _open_peers(self):
+        """IPC-map every other rank's ``out`` (handles exchanged over the group)."""
+        import torch.distributed as dist
+
+        if self.world == 1:
+            return [], []
+        L = _lib.load()
+        handle = (ctypes.c_char * 64)()
+        off = ctypes.c_int64()
+        _lib.check(L.et_ipc_handle(self.out.data_ptr(), ctypes.addressof(handle),
+                                   ctypes.byref(off)))
+        mine = (bytes(handle), off.value)
+        every = [None] * self.world
+        dist.all_gather_object(every, mine, group=self.group)
+        peers, offs = [], []
+        for r, (h, o) in enumerate(every):
+            if r == self.rank:
+                continue
+            hb = (ctypes.c_char * 64).from_buffer_copy(h)
+            ptr = ctypes.c_void_p()
+            _lib.check(L.et_ipc_open(ctypes.addressof(hb), o, ctypes.byref(ptr)))
+            peers.append(ptr.value)
+            offs.append(o)
+        return peers, offs
+
+    def close(self):
+        """Unmap the peers' destinations (p2p exchange)."""
+        if getattr(self, "_peers", None):
+            L = _lib.load()
+            for p, o in zip(self._peers, self._peer_offs):
+                _lib.check(L.et_ipc_close(p, o))
+            self._peers, self._peer_offs = [], []
+
+    def _p2p_barrier(self):
+        """Stream-ordered rendezvous: returns on the current stream once every rank's
+        work queued before it has finished (its pushes, or its use of ``out``)."""
+        import torch.distributed as dist
+
+        if self.world == 1:
+            return
+        if self._gloo():  # ranks sharing one GPU in rehearsal: host-side barrier
+            torch.cuda.current_stream(self.device).synchronize()
+            dist.barrier(group=self.group)
+        else:
+            dist.all_reduce(self._flag, op=dist.ReduceOp.MAX, group=self.group)
+
+    def push_chunk(self, b0: int, b1: int):
+        """et_push_cols: this rank's columns of bags [b0, b1) into every peer's ``out``."""
+        if not self._peers:
+            return
+        L = _lib.load()
+        out = self.out[b0:b1]
+        shift = b0 * _ld(self.out) * out.element_size()  # the chunk's first bag, in every copy
+        shifted = (ctypes.c_void_p * len(self._peers))(*[p + shift for p in self._peers])
+        for dcol, n, _ in self._groups:
+            _lib.check(L.et_push_cols(
+                _lib.et_dtype(out), out.data_ptr(), _ld(self.out), b1 - b0, dcol, n,
+                ctypes.addressof(shifted), len(self._peers), _lib.stream_handle(out.device)))
+
+    def _lookup_p2p(self, piece_tables, piece_idx, b0: int, b1: int):
+        """This rank's lookups for bags [b0, b1), written in place into ``out``."""
+        from .lookup import PreallocationPlan, PreallocationStrategy
+
+        for gi, (dcol, n, members) in enumerate(self._groups):
+            tabs = [piece_tables[m] for m in members]
+            idx = [piece_idx[m] for m in members]
+            key = (gi, b0, b1, tuple((id(t), t.device_table()) for t in tabs),
+                   tuple((i.data_ptr(), tuple(i.shape), tuple(i.stride())) for i in idx))
+            plan = self._plans.get(key)
+            if plan is None:
+                if len(self._plans) >= 64:
+                    self._plans.clear()
+                plan = PreallocationPlan(PreallocationStrategy(0), self.out[b0:b1, dcol:dcol + n],
+                                         tabs, [i[b0:b1] for i in idx])
+                self._plans[key] = plan
+            plan()
+
+    def _call_p2p(self, piece_tables, piece_idx, dst):
+        if dst is not None and dst.data_ptr() != self.out.data_ptr():
+            raise ValueError("the p2p exchange writes into ShardedMapLookup.out (pass it, or None)")
+        main = torch.cuda.current_stream(self.device)
+        # the peers must be done with the previous step's `out` before pushes land in it:
+        # that barrier runs on the exchange stream, beside the first chunk's lookups
+        self._comm.wait_stream(main)
+        with torch.cuda.stream(self._comm):
+            self._p2p_barrier()
+        for c in range(self.chunks):
+            b0, b1 = self.bounds[c], self.bounds[c + 1]
+            self._lookup_p2p(piece_tables, piece_idx, b0, b1)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self._comm.wait_event(ev)
+            with torch.cuda.stream(self._comm):
+                self.push_chunk(b0, b1)
+        main.wait_stream(self._comm)
+        self._p2p_barrier()  # every peer's pushes into this rank's `out` have landed
+        return self.out
 
     # --- the exchange -------------------------------------------------------------------
     def _gloo(self) -> bool:
@@ -317,7 +437,9 @@ class ShardedMapLookup:
 
     def __call__(self, piece_tables, piece_idx, dst: torch.Tensor) -> torch.Tensor:
         """Run the sharded step; ``dst`` is ``(B, k + sum D)`` (allgather) or this
-        rank's ``(B_r, k + sum D)`` batch slice (alltoall)."""
+        rank's ``(B_r, k + sum D)`` batch slice (alltoall); p2p returns ``self.out``."""
+        if self.exchange_kind == "p2p":
+            return self._call_p2p(piece_tables, piece_idx, dst)
         if self.exchange_kind == "alltoall":
             self.lookup_chunk(piece_tables, piece_idx, 0, self.batch)
             self._all_to_all(self.gathered[0], self.slab)
@@ -375,7 +497,7 @@ class ShardedMapLookup:
         from .update import SparseEmbeddingUpdate
 
         ps = self.plan.pieces[self.rank]
-        if self.exchange_kind == "allgather":
+        if self.exchange_kind in ("allgather", "p2p"):
             views = [delta[:, p.col:p.col + p.dim] for p in ps]
         else:
             import torch.distributed as dist

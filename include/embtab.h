@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 3
+#define ET_ABI_VERSION 4
 
 /* Status codes. */
 #define ET_OK 0
@@ -230,6 +230,25 @@ int et_concat_slabs(int dtype, const void* slabs, int32_t nranks, int64_t slab_l
 int et_split_slabs(int dtype, const void* src, int64_t ld_src, int64_t batch, int32_t nranks,
                    const int32_t* rows, const int64_t* src_row_off, void* slabs,
                    int64_t slab_ld, void* stream);
+
+/* One-sided exchange for a sharded maplookup (the "fused P2P xGMI writes" item of
+ * SURVEY.md §8f rank 3; replaces the all-gather + et_concat_slabs of the concat in
+ * src/lookup.jl:316-371 when every rank holds the whole destination): rows
+ * col..col+ncols-1 of every bag of src ((ld x batch), this rank's finished
+ * columns) are stored into the same rows of each peer destination (same ld;
+ * `peers` is a HOST array of npeers device pointers from et_ipc_open).  Publish
+ * with a stream-ordered barrier after the launch. */
+#define ET_MAX_PEERS 16
+int et_push_cols(int dtype, const void* src, int64_t ld, int64_t batch, int64_t col,
+                 int64_t ncols, void* const* peers, int32_t npeers, void* stream);
+
+/* IPC mapping of a device buffer for et_push_cols: et_ipc_handle fills `handle`
+ * (64 bytes) for the allocation holding `ptr` and the byte offset of ptr in it;
+ * another process maps it with et_ipc_open (peer access enabled lazily) and
+ * unmaps it with et_ipc_close(ptr, offset). */
+int et_ipc_handle(const void* ptr, void* handle, int64_t* offset);
+int et_ipc_open(const void* handle, int64_t offset, void** ptr);
+int et_ipc_close(void* ptr, int64_t offset);
 
 /* Deterministic synthetic data (the same counter-based hash as oracle/):
  * element i of dst = lo + (hi-lo) * u(seed, offset + i), u in [0,1) with 24 bits. */
