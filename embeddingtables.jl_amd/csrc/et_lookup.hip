@@ -289,12 +289,11 @@ struct StripeMap {
     uint32_t ntload_mask;  // bit t: non-temporal row loads for table t
 };
 
-template <typename T, typename A, int D, int U, bool NT, bool NTI = false>
-__global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, StripeMap sm,
-                                                            int ntables, int64_t batch,
-                                                            T* __restrict__ dst, int64_t ld_dst,
-                                                            int rounds, int64_t stripe_chunks,
-                                                            int64_t nchunks) {
+template <typename T, typename A, int D, int U, bool NT, bool NTI>
+__device__ __forceinline__ void striped_body(const LookupPack& pack, const StripeMap& sm,
+                                             int ntables, int64_t batch, T* __restrict__ dst,
+                                             int64_t ld_dst, int rounds, int64_t stripe_chunks,
+                                             int64_t nchunks) {
     const int x = blockIdx.x % kXcds;
     const int64_t slot = blockIdx.x / kXcds;
     const int k = (int)(slot % ntables);
@@ -307,6 +306,26 @@ __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, Str
         run_bags<T, A, D, U, NT, true, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
     else
         run_bags<T, A, D, U, NT, false, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+}
+
+template <typename T, typename A, int D, int U, bool NT, bool NTI = false>
+__global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, StripeMap sm,
+                                                            int ntables, int64_t batch,
+                                                            T* __restrict__ dst, int64_t ld_dst,
+                                                            int rounds, int64_t stripe_chunks,
+                                                            int64_t nchunks) {
+    striped_body<T, A, D, U, NT, NTI>(pack, sm, ntables, batch, dst, ld_dst, rounds,
+                                      stripe_chunks, nchunks);
+}
+
+// The same kernel held to 64 VGPRs (8 waves per SIMD instead of 7): ET_W8=1 experiment.
+template <typename T, typename A, int D, int U, bool NT, bool NTI = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void
+k_pooled_vec_striped_w8(LookupPack pack, StripeMap sm, int ntables, int64_t batch,
+                        T* __restrict__ dst, int64_t ld_dst, int rounds, int64_t stripe_chunks,
+                        int64_t nchunks) {
+    striped_body<T, A, D, U, NT, NTI>(pack, sm, ntables, batch, dst, ld_dst, rounds,
+                                      stripe_chunks, nchunks);
 }
 
 // Non-reducing gather (bit copy) of RB-byte rows: each group moves U rows at once.
@@ -477,6 +496,7 @@ struct LookupTuning {
     int max_rounds = 8;                      // ET_ROUNDS: max bag rounds per workgroup
     int64_t light_bytes = 4 << 20; // tables up to one XCD L2 (4 MiB) are "light"
     int rows_in_flight = 0;        // ET_U=4|8|16: rows per group in flight (fp32 D=128)
+    int w8 = 0;                    // ET_W8=1: the striped kernel held to 8 waves per SIMD
 };
 
 inline const LookupTuning& tuning() {
@@ -489,6 +509,7 @@ inline const LookupTuning& tuning() {
         if (const char* e = getenv("ET_ROUNDS")) v.max_rounds = atoi(e) > 0 ? atoi(e) : 1;
         if (const char* e = getenv("ET_LIGHT_BYTES")) v.light_bytes = atoll(e);
         if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
+        if (const char* e = getenv("ET_W8")) v.w8 = atoi(e);
         return v;
     }();
     return t;
@@ -567,7 +588,11 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
         const int64_t grid = (int64_t)kXcds * n * stripe_chunks;
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
-        if (tuning().ntidx && D == 128 && __is_same(T, float))
+        if (tuning().w8 && D == 128 && __is_same(T, float))
+            hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT>), dim3((unsigned)grid),
+                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               ld_dst, rounds, stripe_chunks, nchunks);
+        else if (tuning().ntidx && D == 128 && __is_same(T, float))
             hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT, true>), dim3((unsigned)grid),
                                dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
                                ld_dst, rounds, stripe_chunks, nchunks);

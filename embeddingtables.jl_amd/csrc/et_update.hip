@@ -287,6 +287,14 @@ __device__ __forceinline__ void vec_index(int sub, int vpr, int (&vix)[NV]) {
     }
 }
 
+//
+// Repeated bags.  A row that occurs k times in one bag has k consecutive sorted
+// occurrences with the same bag (the sort is stable and occurrence ids are bag-major),
+// so they all add the same delta column.  Each run of equal bags inside a slice of LPR
+// occurrences is loaded ONCE and added `run` times in a row — the same sequence of
+// fp32 adds as one load per occurrence, bit for bit.  The runs' heads are compacted to
+// the front of the group with a forward lane permute (ds_permute), so the load loop
+// walks heads only (Zipf(1.05) Criteo batch: 25% fewer delta gathers).
 template <int D, int U>
 __device__ __forceinline__ void occ_sum(const float* __restrict__ delta, uint32_t ld_delta,
                                         uint32_t occ_off, uint32_t pool,
@@ -296,19 +304,36 @@ __device__ __forceinline__ void occ_sum(const float* __restrict__ delta, uint32_
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
+    constexpr uint64_t kGroupBits = LPR == 64 ? ~0ull : ((1ull << LPR) - 1);
+    const int lane = g * LPR + sub;
     int vix[NV];
     vec_index<LPR, NV>(sub, vpr, vix);
     for (uint32_t c0 = s0; c0 < s1; c0 += LPR) {
         const int cnt = (int)(s1 - c0 < (uint32_t)LPR ? s1 - c0 : (uint32_t)LPR);
         const uint32_t myo = vals[c0 + (uint32_t)(sub < cnt ? sub : cnt - 1)];
         const int mybag = (int)((myo - occ_off) / pool);
-        for (int i0 = 0; i0 < cnt; i0 += U) {
-            const int m = cnt - i0 < U ? cnt - i0 : U;
+        // run heads of this slice: first slot, or a bag different from the previous slot's
+        const int prev = __shfl(mybag, sub > 0 ? lane - 1 : lane, 64);
+        const bool head = sub < cnt && (sub == 0 || mybag != prev);
+        const uint64_t gm = (LPR == 64 ? (uint64_t)__ballot(head)
+                                       : ((uint64_t)__ballot(head) >> (g * LPR))) & kGroupBits;
+        const int nh = __popcll(gm);
+        const int rank = __popcll(gm & ((1ull << sub) - 1));  // heads before this slot
+        const uint64_t after = sub + 1 < 64 ? gm >> (sub + 1) : 0ull;
+        const int run = (after ? sub + __ffsll((long long)after) : cnt) - sub;
+        // heads to slots [0, nh) in order, the other slots behind them (a permutation)
+        const int to = g * LPR + (head ? rank : nh + (sub - rank));
+        const int hbag = __builtin_amdgcn_ds_permute(to << 2, mybag);
+        const int hrun = __builtin_amdgcn_ds_permute(to << 2, run);
+        for (int i0 = 0; i0 < nh; i0 += U) {
+            const int m = nh - i0 < U ? nh - i0 : U;
             uint64_t off[U];
+            int rep[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int slot = i0 + (u < m ? u : m - 1);
-                const uint32_t bag = (uint32_t)__shfl(mybag, g * LPR + slot, 64);
+                const int slot = g * LPR + i0 + (u < m ? u : m - 1);
+                const uint32_t bag = (uint32_t)__shfl(hbag, slot, 64);
+                rep[u] = __shfl(hrun, slot, 64);
                 off[u] = (uint64_t)bag * ld_delta;
             }
             u32x4 buf[U][NV];
@@ -321,13 +346,15 @@ __device__ __forceinline__ void occ_sum(const float* __restrict__ delta, uint32_
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (u < m) {
+                    for (int k = 0; k < rep[u]; ++k) {
 #pragma unroll
-                    for (int v = 0; v < NV; ++v) {
-                        const u32x4 b = buf[u][v];
-                        acc[v][0] = acc[v][0] + __uint_as_float(b.x);
-                        acc[v][1] = acc[v][1] + __uint_as_float(b.y);
-                        acc[v][2] = acc[v][2] + __uint_as_float(b.z);
-                        acc[v][3] = acc[v][3] + __uint_as_float(b.w);
+                        for (int v = 0; v < NV; ++v) {
+                            const u32x4 b = buf[u][v];
+                            acc[v][0] = acc[v][0] + __uint_as_float(b.x);
+                            acc[v][1] = acc[v][1] + __uint_as_float(b.y);
+                            acc[v][2] = acc[v][2] + __uint_as_float(b.z);
+                            acc[v][3] = acc[v][3] + __uint_as_float(b.w);
+                        }
                     }
                 }
             }

@@ -383,3 +383,23 @@ def test_update_masked_vector_dims(oracle, dim):
                 occ[:, None] * delta.astype(np.float64)).sum(0)
             scale = np.abs(base[8]) + 0.3 * (occ[:, None] * np.abs(delta)).sum(0)
             assert np.all(np.abs(got[8] - exact64) <= 1e-6 * scale)
+
+
+@pytest.mark.parametrize("dim", [16, 32, 64, 128, 256, 512])
+def test_update_repeated_rows_in_bags(oracle, dim):
+    """Tiny tables: every bag repeats its rows many times, so the sorted occurrence
+    lists are long runs of equal bags (one delta load per run, added `run` times) that
+    cross lane-group slices; exact mode bit-identical to the oracle, and an interleaved
+    pattern (runs of length 1) too."""
+    rng = np.random.default_rng(100 + dim)
+    for ncols, B, P in ((3, 257, 40), (7, 130, 70)):
+        base = rng.standard_normal((ncols, dim)).astype(np.float32)
+        delta = rng.standard_normal((B, dim)).astype(np.float32)
+        I = np.sort(rng.integers(1, ncols + 1, (B, P)), axis=1)
+        I[::3] = rng.integers(1, ncols + 1, (I[::3].shape))  # unsorted bags as well
+        ref = base.copy()
+        oracle.sgd(ref, delta, I, 0.25, fused=dim * 4 <= 512)
+        A = et.SimpleEmbedding(dev(base), et.Static(dim))
+        et.update_(et.Descent(0.25), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta),
+                                                                 dev(I)), exact=True)
+        assert bits_equal(host(A.data), ref)
