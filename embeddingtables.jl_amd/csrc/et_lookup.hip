@@ -261,15 +261,184 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Scalar-addressed bag loop for 512-byte rows (D = 128 fp32, 256 f16 / bf16, 64 f64 /
+// i64): LPR = 32, so a wave holds two bags — A in lanes 0-31, B in lanes 32-63 — and
+// both are wave-uniform.  Their index lists are therefore read with SCALAR loads
+// (through the constant address space) and the 64-bit row addresses are formed on the
+// scalar ALU; per row pair the vector ALU only picks one of the two addresses for its
+// half and adds the lane's 16-byte offset.  load_add instead broadcasts every index
+// lane by lane (v_readlane), selects per group, multiplies in 64 bits and selects the
+// zero row per lane — about 20 vector instructions per 1 KiB wave-load that made the
+// L2-resident tables issue-bound.  The summation order is unchanged (pool order from
+// the first row), so results stay bit-identical.  A batch holding an out-of-range
+// index takes a branch that zeroes it per half (rare; undefined in the reference).
+typedef const __attribute__((address_space(4))) int64_t* cidx_ptr;
+
+__device__ __forceinline__ cidx_ptr as_scalar_idx(const int64_t* p) {
+    return (cidx_ptr)(uintptr_t)p;
+}
+
+typedef const __attribute__((address_space(1))) u32x4 gvec16;
+
+// Row offset of a 1-based index v (wave-uniform) in bytes: 32-bit scalar ops only
+// (gfx950's scalar ALU has no 64-bit multiply or ordered 64-bit compare); `bad` gets
+// a nonzero bit unless 1 <= v <= nrows.
+__device__ __forceinline__ uint64_t row_off_s(int64_t v, uint32_t ldb, uint32_t nrows,
+                                              uint32_t& bad) {
+    const uint32_t lo = (uint32_t)v - 1u;
+    // lo < nrows  <=>  the 64-bit difference lo - nrows borrows (all-ones high word);
+    // arithmetic instead of a compare keeps the check on the scalar ALU
+    const uint32_t borrow = (uint32_t)(((uint64_t)lo - (uint64_t)nrows) >> 32);
+    bad |= (uint32_t)((uint64_t)v >> 32) | ~borrow;
+    return (((uint64_t)__umulhi(lo, ldb)) << 32) | (uint64_t)(lo * ldb);
+}
+
+// One batch of UU rows of both bags.  Returns false — before issuing any row load —
+// if an index of the batch is out of range; the caller then redoes the bag pair with
+// bag_pair_checked.
+template <typename T, typename A, int UU, bool NTL>
+__device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t nrows,
+                                           cidx_ptr ia, cidx_ptr ib, uint64_t hmask,
+                                           uint64_t lane_off, bool first_batch,
+                                           A (&acc)[16 / sizeof(T)]) {
+    constexpr int N = 16 / (int)sizeof(T);
+    // lane address = table + row_off(A) + (hi ? row_off(B) - row_off(A) : 0) + 16*sub:
+    // the difference is masked per lane (hmask = ~0 in lanes 32-63), so a row pair costs
+    // two v_and and two 64-bit adds — no 64-bit selects between scalar operands
+    uint64_t oa[UU], dd[UU];
+    uint32_t bad = 0u;
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        oa[u] = row_off_s(ia[u], ldb, nrows, bad);
+        dd[u] = row_off_s(ib[u], ldb, nrows, bad) - oa[u];
+    }
+    if (bad) return false;
+    u32x4 buf[UU];
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        const uint64_t a = ((dd[u] & hmask) + lane_off) + (tb + oa[u]);
+        const gvec16* src = reinterpret_cast<const gvec16*>(a);
+        if constexpr (NTL)
+            buf[u] = __builtin_nontemporal_load(src);
+        else
+            buf[u] = *src;
+    }
+#pragma unroll
+    for (int u = 0; u < UU; ++u) {
+        T x[N];
+        unpack16<T, N>(buf[u], x);
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            if (u == 0)
+                acc[k] = first_batch ? A(x[k]) : A(acc[k] + A(x[k]));
+            else
+                acc[k] = A(acc[k] + A(x[k]));
+        }
+    }
+    return true;
+}
+
+// The bag pair again, one row at a time with per-lane range checks: an out-of-range
+// index contributes a zero row and is counted (the reference leaves it undefined).
+template <typename T, typename A>
+__device__ __forceinline__ void bag_pair_checked(uintptr_t tb, uint32_t ldb,
+                                                           uint32_t nrows, const int64_t* ia,
+                                                           const int64_t* ib, bool hi, int sub,
+                                                           int pool, A* acc, int* bad) {
+    constexpr int N = 16 / (int)sizeof(T);
+    const int64_t* ip = hi ? ib : ia;
+#pragma unroll 1
+    for (int i = 0; i < pool; ++i) {
+        const uint64_t r = (uint64_t)(ip[i] - 1);
+        const bool ok = r < (uint64_t)nrows;
+        *bad += ok ? 0 : 1;
+        const u32x4 v = *(reinterpret_cast<const u32x4*>(
+                              tb + (uint64_t)(ok ? (uint32_t)r : 0u) * ldb) + sub);
+        T x[N];
+        unpack16<T, N>(ok ? v : u32x4{0u, 0u, 0u, 0u}, x);
+        for (int k = 0; k < N; ++k) acc[k] = i == 0 ? A(x[k]) : A(acc[k] + A(x[k]));
+    }
+}
+
+// `rounds` rounds of 8 bags per workgroup (bag mapping identical to run_bags: wave w
+// of round r holds bags chunk*8*rounds + r*8 + 2w + {0, 1}).
+template <typename T, typename A, int U, bool NT, bool NTL>
+__device__ __forceinline__ void run_bags_s(const et_lookup_desc& d, int64_t batch,
+                                           T* __restrict__ dst, int64_t ld_dst, int64_t chunk,
+                                           int rounds) {
+    constexpr int N = 16 / (int)sizeof(T);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool hi = lane >= 32;
+    const int sub = lane & 31;
+    uint32_t hm = hi ? ~0u : 0u;
+    asm volatile("" : "+v"(hm));  // opaque: keep `dd & hmask` two v_and, not selects
+    const uint64_t hmask = ((uint64_t)hm << 32) | hm, lane_off = (uint64_t)sub * 16u;
+    const uintptr_t tb = reinterpret_cast<uintptr_t>(d.table);
+    const uint32_t ldb = (uint32_t)(d.ld_table * (int64_t)sizeof(T)), nr = (uint32_t)d.nrows;
+    const int pool = d.pool;
+    int64_t bag = chunk * 8 * rounds + 2 * wave;
+    for (int r = 0; r < rounds; ++r, bag += 8) {
+        if (bag >= batch) break;
+        const bool has_b = bag + 1 < batch;
+        const cidx_ptr ia = as_scalar_idx(d.idx + bag * d.ld_idx);
+        const cidx_ptr ib = has_b ? as_scalar_idx(d.idx + (bag + 1) * d.ld_idx) : ia;
+        A acc[N];
+#pragma unroll
+        for (int k = 0; k < N; ++k) acc[k] = A(0);
+        bool ok = true;
+        int i0 = 0;
+#define ET_LOAD_ADD_S(UU) \
+    load_add_s<T, A, UU, NTL>(tb, ldb, nr, ia + i0, ib + i0, hmask, lane_off, i0 == 0, acc)
+        for (; ok && i0 + U <= pool; i0 += U) ok = ET_LOAD_ADD_S(U);
+        if constexpr (U > 4) {
+            if (ok && pool - i0 >= 4) {
+                ok = ET_LOAD_ADD_S(4);
+                i0 += 4;
+            }
+        }
+        if constexpr (U > 2) {
+            if (ok && pool - i0 >= 2) {
+                ok = ET_LOAD_ADD_S(2);
+                i0 += 2;
+            }
+        }
+        if (ok && pool - i0 >= 1) ok = ET_LOAD_ADD_S(1);
+#undef ET_LOAD_ADD_S
+        int bad = 0;
+        if (!ok)
+            bag_pair_checked<T, A>(tb, ldb, nr, d.idx + bag * d.ld_idx,
+                                   d.idx + (has_b ? bag + 1 : bag) * d.ld_idx, hi, sub, pool, acc,
+                                   &bad);
+        if (hi && !has_b) bad = 0;  // the upper half re-ran bag A: counted by the lower
+        if (bad && sub == 0) note_oob(bad);
+        if (!hi || has_b) {
+            T y[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) y[k] = T(acc[k]);
+            u32x4* o = reinterpret_cast<u32x4*>(dst + (bag + (hi ? 1 : 0)) * ld_dst +
+                                                d.dst_row_off) + sub;
+            store16<NT>(o, pack16<T, N>(y));
+        }
+    }
+}
+
 // Pooled-sum kernel, vector path: grid = ntables * nchunks workgroups of 256.
-template <typename T, typename A, int D, int U, bool NT, bool PG = false, bool MK = false>
+// SG: the scalar-addressed loop (512-byte rows, contiguous tables, no masking).
+template <typename T, typename A, int D, int U, bool NT, bool PG = false, bool MK = false,
+          bool SG = false>
 __global__ __launch_bounds__(256) void k_pooled_vec(LookupPack pack, int ntables, int64_t batch,
                                                     T* __restrict__ dst, int64_t ld_dst,
                                                     int rounds) {
     const int64_t item = blockIdx.x;
     const int t = (int)(item % ntables);
     const int64_t chunk = item / ntables;
-    run_bags<T, A, D, U, NT, false, false, PG, MK>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    if constexpr (SG)
+        run_bags_s<T, A, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    else
+        run_bags<T, A, D, U, NT, false, false, PG, MK>(pack.d[t], batch, dst, ld_dst, chunk,
+                                                       rounds);
 }
 
 // XCD-aware stripe schedule for multi-table launches.  Every table's chunks are cut
@@ -289,7 +458,7 @@ struct StripeMap {
     uint32_t ntload_mask;  // bit t: non-temporal row loads for table t
 };
 
-template <typename T, typename A, int D, int U, bool NT, bool NTI>
+template <typename T, typename A, int D, int U, bool NT, bool NTI, bool SG = false>
 __device__ __forceinline__ void striped_body(const LookupPack& pack, const StripeMap& sm,
                                              int ntables, int64_t batch, T* __restrict__ dst,
                                              int64_t ld_dst, int rounds, int64_t stripe_chunks,
@@ -302,20 +471,27 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
     const int t = (int)(e & 0xff);
     const int64_t chunk = (int64_t)(e >> 8) * stripe_chunks + j;
     if (j >= stripe_chunks || chunk >= nchunks) return;
-    if ((sm.ntload_mask >> t) & 1u)
-        run_bags<T, A, D, U, NT, true, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
-    else
-        run_bags<T, A, D, U, NT, false, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    if constexpr (SG) {
+        if ((sm.ntload_mask >> t) & 1u)
+            run_bags_s<T, A, U, NT, true>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+        else
+            run_bags_s<T, A, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    } else {
+        if ((sm.ntload_mask >> t) & 1u)
+            run_bags<T, A, D, U, NT, true, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+        else
+            run_bags<T, A, D, U, NT, false, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+    }
 }
 
-template <typename T, typename A, int D, int U, bool NT, bool NTI = false>
+template <typename T, typename A, int D, int U, bool NT, bool NTI = false, bool SG = false>
 __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, StripeMap sm,
                                                             int ntables, int64_t batch,
                                                             T* __restrict__ dst, int64_t ld_dst,
                                                             int rounds, int64_t stripe_chunks,
                                                             int64_t nchunks) {
-    striped_body<T, A, D, U, NT, NTI>(pack, sm, ntables, batch, dst, ld_dst, rounds,
-                                      stripe_chunks, nchunks);
+    striped_body<T, A, D, U, NT, NTI, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
+                                          stripe_chunks, nchunks);
 }
 
 // The same kernel held to 64 VGPRs (8 waves per SIMD instead of 7): ET_W8=1 experiment.
@@ -497,6 +673,7 @@ struct LookupTuning {
     int64_t light_bytes = 4 << 20; // tables up to one XCD L2 (4 MiB) are "light"
     int rows_in_flight = 0;        // ET_U=4|8|16: rows per group in flight (fp32 D=128)
     int w8 = 0;                    // ET_W8=1: the striped kernel held to 8 waves per SIMD
+    int sgpr = 1;                  // ET_SGPR=0: 512-byte rows use the per-lane loop too
 };
 
 inline const LookupTuning& tuning() {
@@ -510,6 +687,7 @@ inline const LookupTuning& tuning() {
         if (const char* e = getenv("ET_LIGHT_BYTES")) v.light_bytes = atoll(e);
         if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
         if (const char* e = getenv("ET_W8")) v.w8 = atoi(e);
+        if (const char* e = getenv("ET_SGPR")) v.sgpr = atoi(e);
         return v;
     }();
     return t;
@@ -582,12 +760,25 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     const int rounds = rounds_for(batch, per_round, n);
     const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
     if (nchunks <= 0) return ET_OK;
+    constexpr bool kSG = !PG && !MK && D * (int)sizeof(T) == 512;
+    bool sg = kSG && tuning().sgpr;  // row strides in bytes must fit 32 bits
+    for (int t = 0; t < n && sg; ++t) sg = pack.d[t].ld_table * (int64_t)sizeof(T) < (1ll << 32);
     if (!PG && !MK && n > 1 && tuning().striped) {
         StripeMap sm;
         build_stripe_map(pack, n, (int)sizeof(T), sm);
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
         const int64_t grid = (int64_t)kXcds * n * stripe_chunks;
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+        if constexpr (kSG) {
+            if (sg) {
+                hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT, false, true>),
+                                   dim3((unsigned)grid), dim3(256), 0, s, pack, sm, n, batch,
+                                   reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
+                                   nchunks);
+                ET_LAUNCH_CHECK("k_pooled_vec_striped");
+                return ET_OK;
+            }
+        }
         if (tuning().w8 && D == 128 && __is_same(T, float))
             hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT>), dim3((unsigned)grid),
                                dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
@@ -606,6 +797,15 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     const int64_t grid = nchunks * n;
     if (grid <= 0) return ET_OK;
     if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+    if constexpr (kSG) {
+        if (sg) {
+            hipLaunchKernelGGL((k_pooled_vec<T, A, D, U, NT, false, false, true>),
+                               dim3((unsigned)grid), dim3(256), 0, s, pack, n, batch,
+                               reinterpret_cast<T*>(dst), ld_dst, rounds);
+            ET_LAUNCH_CHECK("k_pooled_vec");
+            return ET_OK;
+        }
+    }
     hipLaunchKernelGGL((k_pooled_vec<T, A, D, U, NT, PG, MK>), dim3((unsigned)grid), dim3(256), 0, s,
                        pack, n, batch, reinterpret_cast<T*>(dst), ld_dst, rounds);
     ET_LAUNCH_CHECK("k_pooled_vec");

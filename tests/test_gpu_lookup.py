@@ -523,3 +523,47 @@ def test_preallocation_plan_reuse(oracle):
     assert bits_equal(host(dst16[:, k:]), ref16)
     with pytest.raises(et.ArgumentError):
         et.PreallocationPlan(et.PreallocationStrategy(k), dst[:, :100], tabs, idx)
+
+
+@pytest.mark.parametrize("dtype,dim", [(np.float32, 128), (np.float16, 256), (np.float64, 64),
+                                       (np.int64, 64)])
+def test_scalar_addressed_512b_rows(oracle, dtype, dim):
+    """512-byte rows take the scalar-addressed kernel (two bags per wave, index lists
+    read with scalar loads, row addresses on the scalar ALU).  Odd batches (the last
+    wave has no second bag), pools that exercise every batch size (8/4/2/1 rows),
+    single-table and striped multi-table launches, and out-of-range indices —
+    including one whose low word is in range (2^32 + 1) — must match the oracle bit
+    for bit, with bad indices counted and contributing zero rows."""
+    rng = np.random.default_rng(512 + dim)
+    mk = (lambda r: rng.integers(-99, 99, (r, dim)).astype(dtype)) if dtype == np.int64 else \
+        (lambda r: rng.standard_normal((r, dim)).astype(dtype))
+    card = [7, 300, 1, 4099, 50]
+    pools = [1, 2, 13, 20, 33]
+    hs = [mk(r) for r in card]
+    tabs = [table(h) for h in hs]
+    for B in (1, 3, 257):
+        hidx = [rng.integers(1, r + 1, (B, p)) for r, p in zip(card, pools)]
+        et.check_errors()
+        got = host(et.maplookup(et.PreallocationStrategy(5), tabs, [dev(i) for i in hidx]))
+        assert et.check_errors() == 0
+        assert bits_equal(got[:, 5:], oracle.maplookup_prealloc(hs, hidx, prependrows=5)[:, 5:])
+        for h, A, i in zip(hs, tabs, hidx):  # single-table launches (k_pooled_vec)
+            assert bits_equal(host(et.lookup(A, dev(i))), oracle.lookup(h, i))
+    # out-of-range indices: first entry of a bag, mid-batch, in the second bag of a wave,
+    # and a value whose low 32 bits alone would look valid
+    B = 9
+    hidx = [rng.integers(1, r + 1, (B, p)) for r, p in zip(card, pools)]
+    bad = [i.copy() for i in hidx]
+    edits = [(2, 0, 0, 0), (3, 4, 9, card[3] + 1), (4, 1, 20, -3), (3, 7, 0, (1 << 32) + 1),
+             (1, 8, 1, 301)]
+    for t, j, k, v in edits:
+        bad[t][j, k] = v
+    et.check_errors()
+    got = host(et.maplookup(et.PreallocationStrategy(), tabs, [dev(i) for i in bad]))
+    assert et.check_errors() == len(edits)
+    ref = oracle.maplookup_prealloc(hs, hidx)
+    for t, j, k, _ in edits:
+        keep = np.delete(hidx[t][j:j + 1], k, axis=1)
+        ref[j, dim * t:dim * (t + 1)] = (oracle.pooled_sum(hs[t], keep)[0] if keep.size
+                                         else np.zeros(dim, dtype))
+    assert bits_equal(got, ref)
