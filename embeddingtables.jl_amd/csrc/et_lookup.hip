@@ -272,7 +272,11 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
 // zero row per lane — about 20 vector instructions per 1 KiB wave-load that made the
 // L2-resident tables issue-bound.  The summation order is unchanged (pool order from
 // the first row), so results stay bit-identical.  A batch holding an out-of-range
-// index takes a branch that zeroes it per half (rare; undefined in the reference).
+// index is detected before its rows are loaded and the bag pair is redone by
+// bag_pair_checked (rare; undefined behaviour in the reference).  Tried and dropped:
+// touching the next round's index lines with a vector load behind the first batch
+// (so its scalar loads hit L2) — 4% slower on the Criteo mix, 15% on L2-resident
+// tables (in-order vmcnt: the next batch's waits include the prefetch).
 typedef const __attribute__((address_space(4))) int64_t* cidx_ptr;
 
 __device__ __forceinline__ cidx_ptr as_scalar_idx(const int64_t* p) {
@@ -342,10 +346,9 @@ __device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t 
 // The bag pair again, one row at a time with per-lane range checks: an out-of-range
 // index contributes a zero row and is counted (the reference leaves it undefined).
 template <typename T, typename A>
-__device__ __forceinline__ void bag_pair_checked(uintptr_t tb, uint32_t ldb,
-                                                           uint32_t nrows, const int64_t* ia,
-                                                           const int64_t* ib, bool hi, int sub,
-                                                           int pool, A* acc, int* bad) {
+__device__ __forceinline__ void bag_pair_checked(uintptr_t tb, uint32_t ldb, uint32_t nrows,
+                                                 const int64_t* ia, const int64_t* ib, bool hi,
+                                                 int sub, int pool, A* acc, int* bad) {
     constexpr int N = 16 / (int)sizeof(T);
     const int64_t* ip = hi ? ib : ia;
 #pragma unroll 1
