@@ -481,12 +481,18 @@ def main():
         "samples_per_s": B * args.steps / elapsed,
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_pooled_vec<float,float,128,8,NT>",
+            "kernel": "k_pooled_vec_striped<float,float,128,8,NT,0,SG=1> (scalar-addressed)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic_bytes,
+            # fabric-side bytes (PMC, per launch) over the same launch time: how close the
+            # memory system itself runs to the HBM peak (cache-resident tables make the
+            # algorithmic rate exceed it)
+            "traffic_GBs": (traffic_bytes / (kernel_ms * 1e-3) / 1e9) if traffic_bytes else None,
+            "traffic_frac": (traffic_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                             if traffic_bytes else None),
             "algorithmic_bytes_per_launch": local_bytes,
             "kernel_ms": kernel_ms,
             "kernel_ms_median": kernel_ms_median,

@@ -498,13 +498,13 @@ __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, Str
 }
 
 // The same kernel held to 64 VGPRs (8 waves per SIMD instead of 7): ET_W8=1 experiment.
-template <typename T, typename A, int D, int U, bool NT, bool NTI = false>
+template <typename T, typename A, int D, int U, bool NT, bool NTI = false, bool SG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 k_pooled_vec_striped_w8(LookupPack pack, StripeMap sm, int ntables, int64_t batch,
                         T* __restrict__ dst, int64_t ld_dst, int rounds, int64_t stripe_chunks,
                         int64_t nchunks) {
-    striped_body<T, A, D, U, NT, NTI>(pack, sm, ntables, batch, dst, ld_dst, rounds,
-                                      stripe_chunks, nchunks);
+    striped_body<T, A, D, U, NT, NTI, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
+                                          stripe_chunks, nchunks);
 }
 
 // Non-reducing gather (bit copy) of RB-byte rows: each group moves U rows at once.
@@ -773,6 +773,14 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         const int64_t grid = (int64_t)kXcds * n * stripe_chunks;
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
         if constexpr (kSG) {
+            if (sg && tuning().w8) {
+                hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT, false, true>),
+                                   dim3((unsigned)grid), dim3(256), 0, s, pack, sm, n, batch,
+                                   reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
+                                   nchunks);
+                ET_LAUNCH_CHECK("k_pooled_vec_striped");
+                return ET_OK;
+            }
             if (sg) {
                 hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT, false, true>),
                                    dim3((unsigned)grid), dim3(256), 0, s, pack, sm, n, batch,
