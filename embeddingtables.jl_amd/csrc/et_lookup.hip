@@ -276,7 +276,10 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
 // bag_pair_checked (rare; undefined behaviour in the reference).  Tried and dropped:
 // touching the next round's index lines with a vector load behind the first batch
 // (so its scalar loads hit L2) — 4% slower on the Criteo mix, 15% on L2-resident
-// tables (in-order vmcnt: the next batch's waits include the prefetch).
+// tables (in-order vmcnt: the next batch's waits include the prefetch).  Also dropped:
+// pairing a heavy table's stripe with a light one in the two halves of each wave (light
+// rows riding on the heavy rows' latency) — +11% on the Criteo mix: a wave then keeps
+// half as many heavy-table bytes in flight, and the heavy tables are concurrency-bound.
 typedef const __attribute__((address_space(4))) int64_t* cidx_ptr;
 
 __device__ __forceinline__ cidx_ptr as_scalar_idx(const int64_t* p) {

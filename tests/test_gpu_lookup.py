@@ -567,3 +567,31 @@ def test_scalar_addressed_512b_rows(oracle, dtype, dim):
         ref[j, dim * t:dim * (t + 1)] = (oracle.pooled_sum(hs[t], keep)[0] if keep.size
                                          else np.zeros(dim, dtype))
     assert bits_equal(got, ref)
+
+
+@pytest.mark.parametrize("B", [1, 3, 257, 2000])
+def test_striped_heavy_and_light_tables(oracle, B):
+    """Heavy tables (> 4 MiB, one above the 256 MiB non-temporal threshold) beside light
+    ones in one striped scalar-addressed launch, odd batches (the last chunk of every
+    table ends early), out-of-range indices counted — bit-identical to the oracle."""
+    rng = np.random.default_rng(1000 + B)
+    card = [530_000, 9000, 7, 300, 1, 4099, 50, 20_000, 3]
+    hs = [rng.random((r, 128), dtype=np.float32) for r in card]
+    tabs = [table(h) for h in hs]
+    P = 13
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in card]
+    et.check_errors()
+    got = host(et.maplookup(et.PreallocationStrategy(2), tabs, [dev(i) for i in hidx]))
+    assert et.check_errors() == 0
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=2, nthreads=8)
+    assert bits_equal(got[:, 2:], ref[:, 2:])
+    bad = [i.copy() for i in hidx]
+    edits = [(0, B - 1, 12, card[0] + 1), (2, 0, 0, 0), (7, B // 2, 5, -1)]
+    for t, j, k, v in edits:
+        bad[t][j, k] = v
+    got = host(et.maplookup(et.PreallocationStrategy(2), tabs, [dev(i) for i in bad]))
+    assert et.check_errors() == len(edits)
+    for t, j, k, _ in edits:
+        keep = np.delete(hidx[t][j:j + 1], k, axis=1)
+        ref[j, 2 + 128 * t:2 + 128 * (t + 1)] = oracle.pooled_sum(hs[t], keep)[0]
+    assert bits_equal(got[:, 2:], ref[:, 2:])
