@@ -321,7 +321,11 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
             "distinct_rows_U": U, "hottest_row_occurrences": hot,
             "update_algorithmic_bytes": upd_bytes,
             "update_achieved_GBs": upd_bytes / (upd_ms * 1e-3) / 1e9,
-            "update_delta_gather_bytes": occ * DIM * 4}
+            "update_delta_gather_bytes": occ * DIM * 4,
+            # the bytes the gather-by-column algorithm itself moves: one delta column per
+            # occurrence (before the repeated-bag dedupe), the table RMW and the indices
+            "update_gather_inclusive_GBs":
+                (occ * DIM * 4 + 2 * U * DIM * 4 + occ * 8) / (upd_ms * 1e-3) / 1e9}
 
 
 def load_traffic():
