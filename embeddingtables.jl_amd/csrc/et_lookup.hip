@@ -280,6 +280,11 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
 // pairing a heavy table's stripe with a light one in the two halves of each wave (light
 // rows riding on the heavy rows' latency) — +11% on the Criteo mix: a wave then keeps
 // half as many heavy-table bytes in flight, and the heavy tables are concurrency-bound.
+// The same scheme for 256-byte rows (four bags per wave, three masked differences: 10
+// instead of ~30 VALU per KiB) measured slower than load_add (D = 64 fp32, 8 tables,
+// B = 65536: L2-resident 0.248 vs 0.227 ms, HBM 0.539 vs 0.462 ms) — four bags' scalar
+// index loads stall each batch, where load_add prefetches the next bag's indices — so
+// only 512-byte rows take this loop.
 typedef const __attribute__((address_space(4))) int64_t* cidx_ptr;
 
 __device__ __forceinline__ cidx_ptr as_scalar_idx(const int64_t* p) {

@@ -526,11 +526,13 @@ def test_preallocation_plan_reuse(oracle):
 
 
 @pytest.mark.parametrize("dtype,dim", [(np.float32, 128), (np.float16, 256), (np.float64, 64),
-                                       (np.int64, 64)])
-def test_scalar_addressed_512b_rows(oracle, dtype, dim):
-    """512-byte rows take the scalar-addressed kernel (two bags per wave, index lists
-    read with scalar loads, row addresses on the scalar ALU).  Odd batches (the last
-    wave has no second bag), pools that exercise every batch size (8/4/2/1 rows),
+                                       (np.int64, 64), (np.float32, 64), (np.float16, 128),
+                                       (np.float64, 32)])
+def test_scalar_addressed_rows(oracle, dtype, dim):
+    """512-byte rows take the scalar-addressed kernel (two bags per wave, index lists read
+    with scalar loads, row addresses on the scalar ALU); 256-byte rows the per-lane loop
+    beside it.  Batches that are not a multiple of the bags per wave (the last wave
+    re-runs its first bag in the spare groups), pools that exercise every batch size,
     single-table and striped multi-table launches, and out-of-range indices —
     including one whose low word is in range (2^32 + 1) — must match the oracle bit
     for bit, with bad indices counted and contributing zero rows."""
@@ -541,7 +543,7 @@ def test_scalar_addressed_512b_rows(oracle, dtype, dim):
     pools = [1, 2, 13, 20, 33]
     hs = [mk(r) for r in card]
     tabs = [table(h) for h in hs]
-    for B in (1, 3, 257):
+    for B in (1, 3, 6, 257):
         hidx = [rng.integers(1, r + 1, (B, p)) for r, p in zip(card, pools)]
         et.check_errors()
         got = host(et.maplookup(et.PreallocationStrategy(5), tabs, [dev(i) for i in hidx]))
