@@ -664,6 +664,25 @@ struct Grouped {
     uint32_t* vals;
 };
 
+// One sort segment per table, sorted on its own column range (et_sort.hip); returns
+// the number of radix passes.
+inline int sort_segments(const UpdatePack& pack, int ntables, RsSegment* seg) {
+    for (int t = 0; t < ntables; ++t) {
+        const uint32_t nr = (uint32_t)pack.d[t].nrows;
+        seg[t] = RsSegment{pack.occ_off[t], pack.occ_off[t + 1] - pack.occ_off[t],
+                           pack.row_off[t], nr, bits_for(nr)};
+    }
+    return rs_total_passes(seg, ntables);
+}
+
+// Where group_occurrences left the sorted pairs (for an APPLY_ONLY call): buffer a
+// after an even number of radix passes, b after an odd one (segmented_radix_sort).
+inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs& w) {
+    RsSegment seg[ET_MAX_TABLES_PER_LAUNCH];
+    const int P = sort_segments(pack, ntables, seg);
+    return (P & 1) ? Grouped{w.kb, w.vb} : Grouped{w.ka, w.va};
+}
+
 inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s) {
     const int64_t blocks = cdiv64(n, 256);
@@ -678,14 +697,8 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
         kg.blk_off[t + 1] = kg.blk_off[t] + (uint32_t)nb;
     }
     (void)kb_grid;
-    // One sort segment per table, sorted on its own column range (et_sort.hip).
     RsSegment seg[ET_MAX_TABLES_PER_LAUNCH];
-    for (int t = 0; t < ntables; ++t) {
-        const uint32_t nr = (uint32_t)pack.d[t].nrows;
-        seg[t] = RsSegment{pack.occ_off[t], pack.occ_off[t + 1] - pack.occ_off[t],
-                           pack.row_off[t], nr, bits_for(nr)};
-    }
-    const int P = rs_total_passes(seg, ntables);
+    const int P = sort_segments(pack, ntables, seg);
     kg.in_b = 0;
     for (int t = 0; t < ntables; ++t)
         if ((P - rs_passes(seg[t].bits)) & 1) kg.in_b |= 1u << t;
@@ -826,7 +839,7 @@ int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
 }
 
 inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_out,
-                           uint64_t* rows_out, int* pdim_out) {
+                           uint64_t* rows_out, int* pdim_out, bool need_delta = true) {
     if (ntables < 0) return fail(ET_ERR_ARG, "negative ntables");
     if (ntables > ET_MAX_TABLES_PER_LAUNCH)
         return fail(ET_ERR_ARG, "at most %d tables per update call", ET_MAX_TABLES_PER_LAUNCH);
@@ -839,7 +852,8 @@ inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_
         if (d.dim < 0 || d.pool < 0 || d.nrows < 0 || d.batch < 0 || d.cols_per_page < 0)
             return fail(ET_ERR_ARG, "table %d: negative size", t);
         if (d.pool > 0 && d.batch > 0) {
-            if (!d.table || !d.delta || !d.idx) return fail(ET_ERR_ARG, "table %d: NULL", t);
+            if (!d.idx || (need_delta && (!d.table || !d.delta)))
+                return fail(ET_ERR_ARG, "table %d: NULL", t);
             if (d.ld_idx < d.pool) return fail(ET_ERR_ARG, "table %d: ld_idx < pool", t);
             if (d.ld_table < d.dim || d.ld_delta < d.dim)
                 return fail(ET_ERR_ARG, "table %d: leading dimension < dim", t);
@@ -880,10 +894,14 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     et::clear_err();
     if (dtype != ET_F32 && dtype != ET_F64 && dtype != ET_F16 && dtype != ET_BF16)
         return et::fail(ET_ERR_UNSUPPORTED, "sparse SGD: dtype %d", dtype);
+    const bool index_only = (flags & ET_FLAG_SGD_INDEX_ONLY) != 0;
+    const bool apply_only = (flags & ET_FLAG_SGD_APPLY_ONLY) != 0;
+    if (index_only && apply_only)
+        return et::fail(ET_ERR_ARG, "sparse SGD: INDEX_ONLY and APPLY_ONLY both set");
     int64_t n;
     uint64_t rows;
     int pdim;
-    int rc = et::validate_update(descs, ntables, &n, &rows, &pdim);
+    int rc = et::validate_update(descs, ntables, &n, &rows, &pdim, !index_only);
     if (rc != ET_OK) return rc;
     if (n == 0) return ET_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -926,8 +944,12 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     const uint32_t sent = ro;  // key of out-of-range occurrences (sorts last)
 
     et::Grouped gr;
-    rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s);
-    if (rc != ET_OK) return rc;
+    if (apply_only) {
+        gr = et::grouped_pairs(pack, ntables, w);  // phase 1 ran earlier in stream order
+    } else {
+        rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s);
+        if (rc != ET_OK || index_only) return rc;
+    }
 
     const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
     const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;

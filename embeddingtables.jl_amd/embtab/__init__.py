@@ -14,7 +14,7 @@ from .tables import (AbstractEmbeddingTable, AbstractLookupType, ArgumentError, 
 from .lookup import (AbstractExecutionStrategy, DefaultStrategy, NoTangent,
                      PreallocationPlan, PreallocationStrategy, SimpleParallelStrategy, colwrap, destination, lookup,
                      lookup_, maplookup, maplookup_)
-from .update import (AbstractIndexer, DenseIndexer, Descent, Indexer, IndexerView,
+from .update import (AbstractIndexer, DenseIndexer, Descent, Indexer, IndexerView, PhasedUpdate,
                      SparseEmbeddingUpdate, SparseIndexer, ensemble_update, gettranslations,
                      index_, optimise_update_, rrule, uncompress, update_)
 
@@ -28,5 +28,5 @@ __all__ = [
     "lookup", "lookup_", "maplookup", "maplookup_", "SparseEmbeddingUpdate", "uncompress",
     "rrule", "Descent", "AbstractIndexer", "Indexer", "SparseIndexer", "DenseIndexer",
     "IndexerView", "index_", "gettranslations", "update_", "optimise_update_",
-    "ensemble_update", "EmbtabError", "check_errors",
+    "ensemble_update", "PhasedUpdate", "EmbtabError", "check_errors",
 ]

@@ -20,8 +20,10 @@ ET_FLAG_F16_FP32_ACC = 2
 ET_FLAG_EXACT_UPDATE = 4
 ET_FLAG_SGD_UNFUSED = 8
 ET_FLAG_SGD_F64_ALPHA = 16
+ET_FLAG_SGD_INDEX_ONLY = 32
+ET_FLAG_SGD_APPLY_ONLY = 64
 ET_MAX_TABLES_PER_LAUNCH = 32
-ET_ABI_VERSION = 4
+ET_ABI_VERSION = 5
 ET_MAX_PEERS = 16
 
 TORCH_TO_ET = {

@@ -345,6 +345,74 @@ def _update_from_indexer(table, grad: SparseEmbeddingUpdate, indexer: AbstractIn
         _lib.stream_handle(table.device)))
 
 
+class PhasedUpdate:
+    """The multi-table ``update!(opt, tables, grads, indexers)`` split at the reference's
+    own phase boundary (src/sparseupdate.jl:210-213 "index all", then :216-237 "update
+    all"), so the index phase can run while the gradient is still being produced.
+
+    ``index_(stream)`` reads only the index arrays (keys, sort, segments, chunk
+    records into this object's own workspaces); ``update_(opt, stream)`` waits for it
+    and sums the gradient columns and updates the tables.  The gradients' ``delta``
+    tensors are bound at construction (their storage, not their values): fill them
+    before ``update_``.  Results are bit-identical to ``update_(opt, tables, grads,
+    indexers)`` with the same ``exact`` / ``nontemporal`` / ``f16_fp32_acc``."""
+
+    def __init__(self, tables, grads, *, nontemporal: bool = True, exact: bool = False,
+                 f16_fp32_acc: bool = False):
+        tables, grads = list(tables), list(grads)
+        if len(tables) != len(grads):
+            raise ArgumentError("tables and grads differ in length")
+        groups: dict = {}
+        for A, g in zip(tables, grads):
+            if g.indices.numel() == 0:
+                continue
+            groups.setdefault((fused_update_path(A), A.dtype), []).append(_update_desc(A, g))
+        self.device = tables[0].device if tables else None
+        self._keep = (tables, grads)  # the descriptors point into these
+        self._calls = []  # (dtype, desc array, n, flags, workspace)
+        L = _lib.load()
+        for (fused, dtype), descs in groups.items():
+            flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc)
+            for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
+                part = descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH]
+                arr = (_lib.UpdateDesc * len(part))(*part)
+                nb = ctypes.c_int64(0)
+                _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), len(part),
+                                                   ctypes.byref(nb)))
+                ws = torch.empty(max(int(nb.value), 256), dtype=torch.uint8, device=self.device)
+                self._calls.append((dtype, arr, len(part), flags, ws))
+        self._indexed = None
+
+    def _run(self, eta: float, phase: int, stream):
+        L = _lib.load()
+        h = stream.cuda_stream
+        for dtype, arr, n, flags, ws in self._calls:
+            _lib.check(L.et_sparse_sgd(_lib.TORCH_TO_ET[dtype], ctypes.addressof(arr), n,
+                                       float(eta), flags | phase, ws.data_ptr(), ws.numel(), h))
+
+    def index_(self, stream=None):
+        """Phase 1 on ``stream`` (default: the current stream)."""
+        if self.device is None:
+            return self
+        stream = stream or torch.cuda.current_stream(self.device)
+        self._run(0.0, _lib.ET_FLAG_SGD_INDEX_ONLY, stream)
+        self._indexed = torch.cuda.Event()
+        self._indexed.record(stream)
+        return self
+
+    def update_(self, opt: Descent, stream=None):
+        """Phase 2 on ``stream`` (default: the current stream), ordered after the last
+        ``index_``.  May be repeated (same indices, new gradient values)."""
+        if self.device is None:
+            return None
+        if self._indexed is None:
+            raise ArgumentError("PhasedUpdate.update_ before index_")
+        stream = stream or torch.cuda.current_stream(self.device)
+        stream.wait_event(self._indexed)
+        self._run(opt.eta, _lib.ET_FLAG_SGD_APPLY_ONLY, stream)
+        return None
+
+
 def optimise_update_(opt, x, xbar: SparseEmbeddingUpdate, indexer=None, nontemporal=True):
     """``Flux.Optimise.update!(opt, x, xbar::SparseEmbeddingUpdate, ...)``
     (src/sparseupdate.jl:180-189)."""

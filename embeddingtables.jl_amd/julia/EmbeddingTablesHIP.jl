@@ -26,6 +26,8 @@ const ET_F32, ET_F16, ET_F64, ET_I32, ET_I64 = Cint(0), Cint(1), Cint(2), Cint(3
 const ET_FLAG_NONTEMPORAL = UInt32(1)
 const ET_FLAG_SGD_UNFUSED = UInt32(8)
 const ET_FLAG_SGD_F64_ALPHA = UInt32(16)
+const ET_FLAG_SGD_INDEX_ONLY = UInt32(32)   # phase 1 of update!: index all (src/sparseupdate.jl:210-213)
+const ET_FLAG_SGD_APPLY_ONLY = UInt32(64)   # phase 2: update all (:216-237)
 
 et_dtype(::Type{Float32}) = ET_F32
 et_dtype(::Type{Float16}) = ET_F16

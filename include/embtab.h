@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 4
+#define ET_ABI_VERSION 5
 
 /* Status codes. */
 #define ET_OK 0
@@ -73,6 +73,15 @@ extern "C" {
 #define ET_FLAG_SGD_F64_ALPHA 16u /* with ET_FLAG_SGD_UNFUSED: evaluate w - eta*acc in
                                     Float64, as the multi-table generic path does with the
                                     unconverted opt.eta (src/sparseupdate.jl:232) */
+#define ET_FLAG_SGD_INDEX_ONLY 32u /* sparse SGD, phase 1 of 2: only the index work (keys,
+                                    sort, segments, chunk records) into the workspace; reads
+                                    idx, never delta or the tables (delta may be NULL) — the
+                                    reference's "index all" phase, src/sparseupdate.jl:210-213 */
+#define ET_FLAG_SGD_APPLY_ONLY 64u /* sparse SGD, phase 2 of 2: the gradient sums and row
+                                    updates from a workspace that an INDEX_ONLY call with the
+                                    same descriptors, flags and workspace filled earlier in
+                                    stream order ("update all", :216-237); idx is not read
+                                    again, so it may be refilled once phase 1 is done */
 
 /* Tables per launch carried in the kernel-argument segment; longer lists are
  * split into several launches by the library. */

@@ -403,3 +403,73 @@ def test_update_repeated_rows_in_bags(oracle, dim):
         et.update_(et.Descent(0.25), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta),
                                                                  dev(I)), exact=True)
         assert bits_equal(host(A.data), ref)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_phased_update_index_overlapping_forward(oracle, exact):
+    """PhasedUpdate: the index phase (src/sparseupdate.jl:210-213) runs on a side stream
+    while maplookup! runs on the main stream, the update phase (:216-237) after both.
+    Bit-identical to the one-call update_ (hot rows split into chunks, a Dynamic table
+    on the generic path, a Float64 group), the index arrays may be overwritten once the
+    index phase is done, and a second update_ reuses the same index work."""
+    rng = np.random.default_rng(77 + exact)
+    dims, rows, B, P = (128, 64, 40), (2000, 7, 300), 1024, 20
+    hs = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
+    statics = [True, True, False]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    hidx[0][:, :3] = 5  # a hot column: 3072 occurrences, several chunks
+    delta = dev(rng.standard_normal((B, sum(dims))).astype(np.float32))
+    offs = np.cumsum([0] + list(dims[:-1]))
+    h64 = rng.standard_normal((500, 32))
+    i64 = rng.integers(1, 501, (B, 8))
+    d64 = dev(rng.standard_normal((B, 32)))
+
+    def make():
+        tabs = [et.SimpleEmbedding(dev(h), et.Static(h.shape[1]) if s else et.Dynamic)
+                for h, s in zip(hs, statics)]
+        tabs.append(et.SimpleEmbedding(dev(h64), et.Static(32)))
+        idx = [dev(i) for i in hidx] + [dev(i64)]
+        grads = [et.SparseEmbeddingUpdate(t.lookup_type, delta[:, o:o + d], i)
+                 for t, o, d, i in zip(tabs, offs, dims, idx)]
+        grads.append(et.SparseEmbeddingUpdate(tabs[3].lookup_type, d64, idx[3]))
+        return tabs, idx, grads
+
+    opt = et.Descent(0.05)
+    ref_tabs, _, ref_grads = make()
+    et.update_(opt, ref_tabs, ref_grads, None, exact=exact)
+    et.update_(opt, ref_tabs, ref_grads, None, exact=exact)
+
+    tabs, idx, grads = make()
+    pu = et.PhasedUpdate(tabs, grads, exact=exact)
+    out = torch.empty((B, sum(dims)), dtype=torch.float32, device=DEV)
+    main = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+    side.wait_stream(main)
+    pu.index_(side)
+    et.maplookup_(et.PreallocationStrategy(0), out, tabs[:3], idx[:3])  # concurrent
+    main.wait_stream(side)
+    for i in idx:
+        i.fill_(1)  # phase 2 never reads the indices again
+    pu.update_(opt)
+    pu.update_(opt)
+    torch.cuda.synchronize()
+    for t, (a, b) in enumerate(zip(tabs, ref_tabs)):
+        assert torch.equal(a.data, b.data), f"table {t}"
+    if exact:
+        from embtab.tables import fused_update_path
+
+        refs = [h.copy() for h in hs]
+        hd = host(delta)
+        for _ in range(2):
+            oracle.sgd_multi(refs, hd, hidx, 0.05, [fused_update_path(t) for t in tabs[:3]],
+                             num_splits=4, nthreads=4, delta_offsets=offs)
+        for t in range(3):
+            assert bits_equal(host(tabs[t].data), refs[t]), f"table {t} vs oracle"
+
+
+def test_phased_update_requires_index_phase():
+    tab = et.SimpleEmbedding(dev(np.ones((10, 16), np.float32)), et.Static(16))
+    g = et.SparseEmbeddingUpdate(tab.lookup_type, torch.ones((4, 16), device=DEV),
+                                 dev(np.ones((4, 2), np.int64)))
+    with pytest.raises(et.ArgumentError):
+        et.PhasedUpdate([tab], [g]).update_(et.Descent(0.1))
