@@ -181,6 +181,7 @@ struct ChunkRec {
     uint32_t s0, s1, key, dst;
 };
 constexpr uint32_t kApply = 0xffffffffu;
+constexpr uint32_t kRetired = 0xffffffffu;  // an mlist entry taken by the hot-column pass
 
 __global__ __launch_bounds__(256) void k_chunk_records(
     const uint32_t* __restrict__ chunk_start, const uint32_t* __restrict__ seg_start,
@@ -477,6 +478,7 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
     {
         for (uint32_t k = blockIdx.x; k < M; k += gridDim.x) {
             const uint32_t seg = mlist[k];
+            if (seg == kRetired) continue;  // a hot column (k_hot_pick), uniform
             {
                 const uint32_t key0 = keys[seg_start[seg]];
                 if (key0 == sent || !((my_mask >> table_of_key(pack, ntables, key0)) & 1u))
@@ -546,6 +548,245 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
             __syncthreads();
         }
     }
+}
+
+// Hot-column pass (non-exact Float32 mode, dim 128, pool <= 32).  The columns with the
+// longest occurrence lists of a table — up to kHotSlots of them, chosen by a per-table
+// length threshold (a log2 histogram of the multi-chunk segments, so the choice never
+// depends on atomic arrival order) — are summed bag-major instead of by gathering one Δ
+// column per (column, bag) pair: workgroup (window, table) streams the Δ columns of
+// kHotWin consecutive bags once, maps each index to its hot slot through an LDS hash, and
+// adds Δ into the slot's LDS accumulator.  Wave w owns the slots s with s % 4 == w and
+// walks the bags and pool positions in order, so every (slot, feature) sum runs in
+// occurrence order from +0; the per-window partials are added in window order by
+// k_hot_combine, which applies the update.  The chunk and combine passes skip the hot
+// columns (their records and list entries are retired by k_hot_pick).
+constexpr int kHotSlots = 120;   // per table (slot ids fit a byte; 0xff = not hot)
+constexpr int kHotWin = 1024;    // bags per workgroup (one partial per window)
+constexpr int kHotBatch = 32;    // bags staged in LDS at a time
+constexpr int kHotHash = 256;    // open-addressing LDS hash of the hot keys
+constexpr int kHotMaxPool = 32;
+
+struct HotList {
+    int n;
+    int t[ET_MAX_TABLES_PER_LAUNCH];
+    uint64_t soff[ET_MAX_TABLES_PER_LAUNCH];  // the table's slot bytes in the workspace
+};
+
+__global__ __launch_bounds__(256) void k_hot_hist(UpdatePack pack, int ntables, uint32_t hot_mask,
+                                                  const uint32_t* __restrict__ keys,
+                                                  const uint32_t* __restrict__ seg_start,
+                                                  const uint32_t* __restrict__ mlist,
+                                                  const uint32_t* __restrict__ counters,
+                                                  uint32_t* __restrict__ hist) {
+    const uint32_t M = counters[kCntM];
+    for (uint32_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
+        const uint32_t u = mlist[m];
+        const uint32_t ss = seg_start[u], len = seg_start[u + 1] - ss, key = keys[ss];
+        if (key >= pack.row_off[ntables]) continue;  // out-of-range occurrences
+        const int t = table_of_key(pack, ntables, key);
+        if (!((hot_mask >> t) & 1u)) continue;
+        atomicAdd(&hist[t * 32 + (31 - __builtin_clz(len))], 1u);
+    }
+}
+
+__device__ __forceinline__ int hot_threshold(const uint32_t* __restrict__ hist, int t) {
+    // smallest log2 bucket b with (segments of length >= 2^b) <= kHotSlots
+    uint32_t acc = 0;
+    int b0 = 32;
+    for (int b = 31; b >= 0; --b) {
+        acc += hist[t * 32 + b];
+        if (acc > (uint32_t)kHotSlots) break;
+        b0 = b;
+    }
+    return b0;
+}
+
+__global__ __launch_bounds__(256) void k_hot_pick(UpdatePack pack, int ntables, uint32_t hot_mask,
+                                                  const uint32_t* __restrict__ keys,
+                                                  const uint32_t* __restrict__ seg_start,
+                                                  const uint32_t* __restrict__ chunk_start,
+                                                  uint32_t* __restrict__ mlist,
+                                                  const uint32_t* __restrict__ counters,
+                                                  const uint32_t* __restrict__ hist,
+                                                  uint32_t* __restrict__ hcnt,
+                                                  uint32_t* __restrict__ hkey,
+                                                  ChunkRec* __restrict__ recs, uint32_t sent) {
+    const uint32_t M = counters[kCntM];
+    for (uint32_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
+        const uint32_t u = mlist[m];
+        const uint32_t ss = seg_start[u], len = seg_start[u + 1] - ss, key = keys[ss];
+        if (key >= pack.row_off[ntables]) continue;
+        const int t = table_of_key(pack, ntables, key);
+        if (!((hot_mask >> t) & 1u)) continue;
+        if (31 - __builtin_clz(len) < hot_threshold(hist, t)) continue;
+        const uint32_t s = atomicAdd(&hcnt[t], 1u);  // slot ids only place the sums
+        hkey[t * kHotSlots + s] = key;
+        mlist[m] = kRetired;
+        for (uint32_t c = chunk_start[u], ce = chunk_start[u + 1]; c < ce; ++c) recs[c].key = sent;
+    }
+}
+
+__device__ __forceinline__ uint32_t hot_hash(uint32_t key) {
+    return (key * 2654435761u) >> 24;  // kHotHash = 256 buckets
+}
+
+// Index phase: the hot slot of every occurrence of a hot table (0xff: not hot or out of
+// range), one byte each, bag rows padded to P4 = roundup(pool, 4) bytes so the update
+// phase reads a batch of bags as whole words and never touches the indices.
+constexpr int kHotSlotBags = 256;  // bags per workgroup of k_hot_slots
+
+__global__ __launch_bounds__(256) void k_hot_slots(UpdatePack pack, HotList hl,
+                                                   const uint32_t* __restrict__ hcnt,
+                                                   const uint32_t* __restrict__ hkey,
+                                                   uint8_t* __restrict__ slots) {
+    __shared__ uint32_t hk[kHotHash];
+    __shared__ uint8_t hs[kHotHash];
+    const int hi = blockIdx.y, t = hl.t[hi];
+    const et_update_desc& d = pack.d[t];
+    const int64_t bb = (int64_t)blockIdx.x * kHotSlotBags;
+    if (bb >= d.batch) return;  // uniform
+    const int nbag = d.batch - bb < kHotSlotBags ? (int)(d.batch - bb) : kHotSlotBags;
+    const uint32_t H = hcnt[t];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kHotHash; i += 256) hk[i] = 0u;
+    __syncthreads();
+    if (tid < (int)H) {
+        const uint32_t key = hkey[t * kHotSlots + tid];
+        uint32_t h = hot_hash(key);
+        while (atomicCAS(&hk[h], 0u, key + 1u) != 0u) h = (h + 1) & (kHotHash - 1);
+        hs[h] = (uint8_t)tid;
+    }
+    __syncthreads();
+    const int P = d.pool, P4 = (P + 3) & ~3, W = P4 / 4;
+    const uint32_t r0 = pack.row_off[t];
+    const uint64_t nrows = (uint64_t)d.nrows;
+    uint32_t* out = reinterpret_cast<uint32_t*>(slots + hl.soff[hi] + (uint64_t)bb * P4);
+    for (int e = tid; e < nbag * W; e += 256) {
+        const int j = e / W, i0 = (e % W) * 4;
+        const int64_t* ip = d.idx + (bb + j) * d.ld_idx;
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t sv = 0xffu;
+            const int i = i0 + b;
+            if (i < P && H > 0) {
+                const int64_t x = ip[i];
+                if (x >= 1 && (uint64_t)x <= nrows) {
+                    const uint32_t key = r0 + (uint32_t)(x - 1);
+                    uint32_t h = hot_hash(key);
+                    for (;;) {
+                        const uint32_t v = hk[h];
+                        if (v == key + 1u) {
+                            sv = hs[h];
+                            break;
+                        }
+                        if (v == 0u) break;
+                        h = (h + 1) & (kHotHash - 1);
+                    }
+                }
+            }
+            word |= sv << (8 * b);
+        }
+        out[e] = word;
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void k_sgd_hot(UpdatePack pack, HotList hl,
+                                                    const uint32_t* __restrict__ hcnt,
+                                                    const uint8_t* __restrict__ slots,
+                                                    float2* __restrict__ part, int nw) {
+    __shared__ float2 acc[kHotSlots][64];
+    __shared__ float2 dl[kHotBatch][64];
+    __shared__ uint32_t sl[kHotBatch * kHotMaxPool / 4];
+    const int hi = blockIdx.y, t = hl.t[hi];
+    const et_update_desc& d = pack.d[t];
+    const int64_t B = d.batch;
+    const int64_t b0 = (int64_t)blockIdx.x * kHotWin;
+    const uint32_t H = hcnt[t];
+    if (b0 >= B || H == 0) return;  // uniform
+    const int64_t b1 = b0 + kHotWin < B ? b0 + kHotWin : B;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int P = d.pool, P4 = (P + 3) & ~3, W = P4 / 4;
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(slots + hl.soff[hi]);
+    for (int i = tid; i < kHotSlots * 64; i += 256) acc[i >> 6][i & 63] = make_float2(0.0f, 0.0f);
+
+    const float* delta = reinterpret_cast<const float*>(d.delta);
+    const int64_t ldd = d.ld_delta;
+    float2 rd[8];
+    uint32_t rs;
+    auto load = [&](int64_t bb) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t b = bb + wv + 4 * k;
+            rd[k] = b < b1 ? *reinterpret_cast<const float2*>(delta + b * ldd + 2 * lane)
+                           : make_float2(0.0f, 0.0f);
+        }
+        // the batch's slot words: kHotBatch * W <= 256, one per thread
+        rs = (tid < kHotBatch * W && bb + tid / W < b1) ? sw[bb * W + tid] : 0xffffffffu;
+    };
+    load(b0);
+    for (int64_t bb = b0; bb < b1; bb += kHotBatch) {
+        const int nbag = b1 - bb < kHotBatch ? (int)(b1 - bb) : kHotBatch;
+        __syncthreads();  // the previous batch is processed
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dl[wv + 4 * k][lane] = rd[k];
+        if (tid < kHotBatch * W) sl[tid] = rs;
+        __syncthreads();
+        if (bb + kHotBatch < b1) load(bb + kHotBatch);
+        for (int j = 0; j < nbag; ++j) {
+            const float2 dv = dl[j][lane];
+            for (int q = 0; q < W; ++q) {
+                const uint32_t v = __builtin_amdgcn_readfirstlane(sl[j * W + q]);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t s = (v >> (8 * b)) & 0xffu;
+                    if (s != 0xffu && (s & 3u) == (uint32_t)wv) {
+                        float2 a = acc[s][lane];
+                        a.x = a.x + dv.x;
+                        a.y = a.y + dv.y;
+                        acc[s][lane] = a;
+                    }
+                }
+            }
+        }
+    }
+    // window partials, slot-major: part[(hi*kHotSlots + s)*nw + window][64]
+    for (uint32_t s = wv; s < H; s += 4)
+        part[((uint64_t)(hi * kHotSlots + s) * nw + blockIdx.x) * 64 + lane] = acc[s][lane];
+}
+
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl,
+                                                     const uint32_t* __restrict__ hcnt,
+                                                     const uint32_t* __restrict__ hkey,
+                                                     const float2* __restrict__ part, int nw,
+                                                     float eta32, double eta64) {
+    const int lane = threadIdx.x & 63;
+    const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int hi = gw / kHotSlots, s = gw % kHotSlots;
+    if (hi >= hl.n) return;
+    const int t = hl.t[hi];
+    if ((uint32_t)s >= hcnt[t]) return;
+    const et_update_desc& d = pack.d[t];
+    const int nwt = (int)((d.batch + kHotWin - 1) / kHotWin);
+    const float2* p = part + (uint64_t)(hi * kHotSlots + s) * nw * 64 + lane;
+    float ax = 0.0f, ay = 0.0f;
+    for (int w0 = 0; w0 < nwt; w0 += 8) {
+        float2 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = p[(uint64_t)(w0 + k < nwt ? w0 + k : nwt - 1) * 64];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (w0 + k < nwt) {
+                ax = ax + v[k].x;
+                ay = ay + v[k].y;
+            }
+    }
+    const uint32_t key = hkey[t * kHotSlots + s];
+    float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, key - pack.row_off[t]) + 2 * lane;
+    store_scalar<NT>(w, sgd_apply<MODE>(w[0], ax, eta32, eta64));
+    store_scalar<NT>(w + 1, sgd_apply<MODE>(w[1], ay, eta32, eta64));
 }
 
 // Generic kernels (any dim / alignment / element type): one wave per chunk or
@@ -620,6 +861,12 @@ struct UpdateWs {
         *mlist;
     ChunkRec* recs;
     float* partials;
+    // hot-column pass: per-table log2 histograms [32][32] then slot counts [32] (one
+    // memset), hot keys [32][kHotSlots], window partials [nhot][kHotSlots][nw][64] float2
+    uint32_t *hot_hist, *hot_cnt, *hot_key;
+    float2* hot_part;
+    uint8_t* hot_slots;  // [sum over hot-shaped tables of batch * roundup(pool, 4)]
+    int hot_nw;
     int64_t bytes;
 };
 
@@ -627,7 +874,8 @@ inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
 
 // Lay out (or size, when base == nullptr) the update workspace for n occurrences and
 // partial rows of pdim floats.
-inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk) {
+inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
+                                int nhot = 0, int64_t hot_batch = 0, int64_t hot_bytes = 0) {
     UpdateWs w;
     int64_t off = 0;
     auto take = [&](int64_t bytes) -> char* {
@@ -654,6 +902,19 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk)
     const int64_t max_partials = 2 * (n / chunk) + 2;
     // 8 bytes per partial element: float (vector path / fp32 accumulators) or double
     w.partials = (float*)take(8 * max_partials * (int64_t)(pdim > 0 ? pdim : 1));
+    w.hot_nw = (int)((hot_batch + kHotWin - 1) / kHotWin);
+    w.hot_hist = nullptr;
+    w.hot_cnt = nullptr;
+    w.hot_key = nullptr;
+    w.hot_part = nullptr;
+    w.hot_slots = nullptr;
+    if (nhot > 0 && w.hot_nw > 0) {
+        w.hot_slots = (uint8_t*)take(hot_bytes);
+        w.hot_hist = (uint32_t*)take(4 * (32 * 32 + 32));
+        w.hot_cnt = w.hot_hist ? w.hot_hist + 32 * 32 : nullptr;
+        w.hot_key = (uint32_t*)take(4 * 32 * kHotSlots);
+        w.hot_part = (float2*)take((int64_t)nhot * kHotSlots * w.hot_nw * 64 * 8);
+    }
     w.bytes = off;
     return w;
 }
@@ -684,7 +945,8 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
 }
 
 inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
-                             uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s) {
+                             uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s,
+                             uint32_t hot_mask = 0, const HotList* hl = nullptr) {
     const int64_t blocks = cdiv64(n, 256);
     const unsigned kb_grid = (unsigned)(blocks < 65536 ? blocks : 65536);
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
@@ -734,6 +996,20 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chunk_records_multi, dim3(512), dim3(256), 0, s, w.nch, w.seg_start,
                        w.multi, out.keys, w.mlist, chunk, w.counters, w.recs);
     ET_LAUNCH_CHECK("k_chunk_records");
+    if (hot_mask && w.hot_hist && hl && hl->n > 0) {
+        ET_HIP_CHECK(hipMemsetAsync(w.hot_hist, 0, 4 * (32 * 32 + 32), s));
+        hipLaunchKernelGGL(k_hot_hist, dim3(256), dim3(256), 0, s, pack, ntables, hot_mask,
+                           out.keys, w.seg_start, w.mlist, w.counters, w.hot_hist);
+        hipLaunchKernelGGL(k_hot_pick, dim3(256), dim3(256), 0, s, pack, ntables, hot_mask,
+                           out.keys, w.seg_start, w.nch, w.mlist, w.counters, w.hot_hist,
+                           w.hot_cnt, w.hot_key, w.recs, sent);
+        ET_LAUNCH_CHECK("k_hot_pick");
+        hipLaunchKernelGGL(k_hot_slots,
+                           dim3((unsigned)cdiv64(w.hot_nw * (int64_t)kHotWin, kHotSlotBags),
+                                (unsigned)hl->n),
+                           dim3(256), 0, s, pack, *hl, w.hot_cnt, w.hot_key, w.hot_slots);
+        ET_LAUNCH_CHECK("k_hot_slots");
+    }
     return ET_OK;
 }
 
@@ -759,12 +1035,22 @@ struct VecGroups {
 template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
-                     const VecGroups& vg, bool any_generic, hipStream_t s) {
+                     const VecGroups& vg, bool any_generic, hipStream_t s,
+                     const HotList& hl) {
     static const unsigned grid = [] {
         const char* e = getenv("ET_SGD_GRID");  // experiments: workgroups of the SGD passes
         return e ? (unsigned)atoi(e) : 256u * 16u;
     }();
     if constexpr (__is_same(T, float)) {
+        if (hl.n > 0 && w.hot_part) {
+            hipLaunchKernelGGL(k_sgd_hot, dim3((unsigned)w.hot_nw, (unsigned)hl.n), dim3(256), 0, s,
+                               pack, hl, w.hot_cnt, w.hot_slots, w.hot_part, w.hot_nw);
+            hipLaunchKernelGGL((k_hot_combine<MODE, NT>),
+                               dim3((unsigned)cdiv64((int64_t)hl.n * kHotSlots, 4)), dim3(256), 0,
+                               s, pack, hl, w.hot_cnt, w.hot_key, w.hot_part, w.hot_nw,
+                               (float)eta_c, eta64);
+            ET_LAUNCH_CHECK("k_sgd_hot");
+        }
 #define ET_SGD_VEC(DD)                                                                         \
     case DD:                                                                                   \
         hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
@@ -822,10 +1108,11 @@ inline double convert_eta(int dtype, double eta) {
 template <typename T, typename C>
 int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, double eta_c, double eta64,
-                     int mode, bool nt, const VecGroups& vg, bool any_generic, hipStream_t s) {
+                     int mode, bool nt, const VecGroups& vg, bool any_generic, hipStream_t s,
+                     const HotList& hl) {
 #define ET_SGD_CALL(M, NTV)                                                                \
     return launch_sgd_typed<T, C, M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, (C)eta_c, \
-                                          eta64, vg, any_generic, s)
+                                          eta64, vg, any_generic, s, hl)
     if (mode == 0) {
         if (nt) ET_SGD_CALL(0, true);
         ET_SGD_CALL(0, false);
@@ -836,6 +1123,26 @@ int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     if (nt) ET_SGD_CALL(2, true);
     ET_SGD_CALL(2, false);
 #undef ET_SGD_CALL
+}
+
+// Tables the hot-column pass can take (the workspace is sized for all of them).
+inline bool hot_shape(const et_update_desc& d) {
+    return d.dim == 128 && d.pool >= 1 && d.pool <= kHotMaxPool && d.batch > 0;
+}
+
+// Hot-shaped tables: their count, largest batch, and slot-byte offsets (soff[t]) / total.
+inline void hot_sizes(const et_update_desc* descs, int ntables, int* nhot, int64_t* batch,
+                      int64_t* bytes, uint64_t* soff = nullptr) {
+    *nhot = 0;
+    *batch = 0;
+    *bytes = 0;
+    for (int t = 0; t < ntables; ++t)
+        if (hot_shape(descs[t])) {
+            ++*nhot;
+            if (descs[t].batch > *batch) *batch = descs[t].batch;
+            if (soff) soff[t] = (uint64_t)*bytes;
+            *bytes += descs[t].batch * ((descs[t].pool + 3) & ~3);
+        }
 }
 
 inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_out,
@@ -885,7 +1192,10 @@ extern "C" int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntable
     int pdim;
     int rc = et::validate_update(descs, ntables, &n, &rows, &pdim);
     if (rc != ET_OK) return rc;
-    *bytes = et::carve_update_ws(nullptr, n, pdim, et::kChunk).bytes;
+    int nhot;
+    int64_t hb, hbytes;
+    et::hot_sizes(descs, ntables, &nhot, &hb, &hbytes);
+    *bytes = et::carve_update_ws(nullptr, n, pdim, et::kChunk, nhot, hb, hbytes).bytes;
     return ET_OK;
 }
 
@@ -908,7 +1218,12 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     const bool exact = (flags & ET_FLAG_EXACT_UPDATE) != 0;
     // In exact mode a chunk spans a whole segment (n occurrences at most).
     const uint32_t chunk = exact ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff) : et::kChunk;
-    et::UpdateWs w = et::carve_update_ws(static_cast<char*>(workspace), n, pdim, et::kChunk);
+    int nhot;
+    int64_t hb, hbytes;
+    uint64_t soff[ET_MAX_TABLES_PER_LAUNCH];
+    et::hot_sizes(descs, ntables, &nhot, &hb, &hbytes, soff);
+    et::UpdateWs w = et::carve_update_ws(static_cast<char*>(workspace), n, pdim, et::kChunk,
+                                         nhot, hb, hbytes);
     if (!workspace || ws_bytes < w.bytes)
         return et::fail(ET_ERR_WORKSPACE, "workspace of %lld bytes needed",
                         (long long)w.bytes);
@@ -917,6 +1232,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     uint32_t ro = 0, oo = 0;
     et::VecGroups vg;
     bool any_generic = false;
+    uint32_t hot_mask = 0;
     pack.vec_mask = 0;
     for (int t = 0; t < ntables; ++t) {
         const et_update_desc& d = descs[t];
@@ -935,6 +1251,11 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
                             vg.add(cap, t);
         if (vec_ok) {
             pack.vec_mask |= 1u << t;
+            // hot-column pass: Float32 vector tables of dim 128, non-exact mode, float2
+            // gradient loads (identical in both phases for the same descriptors)
+            if (!exact && (flags & ET_FLAG_SGD_HOT_PASS) && et::hot_shape(d) &&
+                (reinterpret_cast<uintptr_t>(d.delta) & 7u) == 0 && d.ld_delta % 2 == 0)
+                hot_mask |= 1u << t;
         } else {
             any_generic = true;
         }
@@ -943,11 +1264,18 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     pack.occ_off[ntables] = oo;
     const uint32_t sent = ro;  // key of out-of-range occurrences (sorts last)
 
+    et::HotList hl;
+    hl.n = 0;
+    for (int t = 0; t < ntables; ++t)
+        if ((hot_mask >> t) & 1u) {
+            hl.soff[hl.n] = soff[t];
+            hl.t[hl.n++] = t;
+        }
     et::Grouped gr;
     if (apply_only) {
         gr = et::grouped_pairs(pack, ntables, w);  // phase 1 ran earlier in stream order
     } else {
-        rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s);
+        rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s, hot_mask, &hl);
         if (rc != ET_OK || index_only) return rc;
     }
 
@@ -958,23 +1286,23 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         case ET_F32:
             return et::launch_sgd_dtype<float, float>(pack, ntables, gr, w, chunk, pdim, sent,
                                                       eta_c, eta, mode, nt, vg,
-                                                      any_generic, s);
+                                                      any_generic, s, hl);
         case ET_F64:
             return et::launch_sgd_dtype<double, double>(pack, ntables, gr, w, chunk, pdim, sent,
                                                          eta_c, eta, mode, nt, vg,
-                                                         any_generic, s);
+                                                         any_generic, s, hl);
         case ET_BF16:
             return et::launch_sgd_dtype<__bf16, float>(pack, ntables, gr, w, chunk, pdim, sent,
                                                        eta_c, eta, mode, nt, vg,
-                                                       any_generic, s);
+                                                       any_generic, s, hl);
         default:  // ET_F16
             if (flags & ET_FLAG_F16_FP32_ACC)
                 return et::launch_sgd_dtype<_Float16, float>(pack, ntables, gr, w, chunk, pdim,
                                                              sent, eta_c, eta, mode, nt, vg,
-                                                             any_generic, s);
+                                                             any_generic, s, hl);
             return et::launch_sgd_dtype<_Float16, _Float16>(pack, ntables, gr, w, chunk, pdim,
                                                             sent, eta_c, eta, mode, nt, vg,
-                                                            any_generic, s);
+                                                            any_generic, s, hl);
     }
 }
 

@@ -22,6 +22,7 @@ ET_FLAG_SGD_UNFUSED = 8
 ET_FLAG_SGD_F64_ALPHA = 16
 ET_FLAG_SGD_INDEX_ONLY = 32
 ET_FLAG_SGD_APPLY_ONLY = 64
+ET_FLAG_SGD_HOT_PASS = 128
 ET_MAX_TABLES_PER_LAUNCH = 32
 ET_ABI_VERSION = 5
 ET_MAX_PEERS = 16

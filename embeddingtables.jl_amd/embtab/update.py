@@ -210,8 +210,10 @@ _UPDATE_DTYPES = (torch.float32, torch.float64, torch.float16, torch.bfloat16)
 
 
 def _sgd_flags(fused: bool, nontemporal: bool, f64_alpha: bool = False, exact: bool = False,
-               f16_fp32_acc: bool = False):
+               f16_fp32_acc: bool = False, hot_pass: bool = False):
     flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
+    if hot_pass:
+        flags |= _lib.ET_FLAG_SGD_HOT_PASS
     if f16_fp32_acc:
         flags |= _lib.ET_FLAG_F16_FP32_ACC
     if not fused:
@@ -254,7 +256,7 @@ def _sparse_sgd(descs, eta: float, flags: int, device, dtype=torch.float32):
 
 
 def update_(*args, nontemporal: bool | None = None, exact: bool = False,
-            f16_fp32_acc: bool = False, **kw):
+            f16_fp32_acc: bool = False, hot_pass: bool = False, **kw):
     """Julia's ``update!`` (multiple dispatch on the argument types):
 
     * ``update_(opt::Descent, table, grad, [indexer], [nontemporal])`` — single table,
@@ -267,17 +269,20 @@ def update_(*args, nontemporal: bool | None = None, exact: bool = False,
     ``exact=True`` sums every column's gradient serially (bit-identical to the
     reference even for hot columns); the default splits occurrence lists longer than
     512 into partial sums combined in a fixed order (deterministic).  Float16 tables
-    use Julia's Float16 arithmetic unless ``f16_fp32_acc`` (sums in Float32)."""
+    use Julia's Float16 arithmetic unless ``f16_fp32_acc`` (sums in Float32).
+    ``hot_pass=True`` (experimental, ET_FLAG_SGD_HOT_PASS) sums the longest occurrence
+    lists of Float32 dim-128 tables bag-major (deterministic, not bit-identical to the
+    default split)."""
     if args and isinstance(args[0], Descent):
         opt = args[0]
         if isinstance(args[1], AbstractEmbeddingTable):
             table, grad = args[1], args[2]
             nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
-            _update_single(opt, table, grad, nt, exact, f16_fp32_acc)
+            _update_single(opt, table, grad, nt, exact, f16_fp32_acc, hot_pass)
             return None
         tables, grads = list(args[1]), list(args[2])
         nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
-        _update_multi(opt, tables, grads, nt, exact, f16_fp32_acc, **kw)
+        _update_multi(opt, tables, grads, nt, exact, f16_fp32_acc, hot_pass=hot_pass, **kw)
         return None
     table, grad, indexer, alpha = args[:4]
     nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
@@ -286,19 +291,20 @@ def update_(*args, nontemporal: bool | None = None, exact: bool = False,
 
 
 def _update_single(opt: Descent, table, grad: SparseEmbeddingUpdate, nontemporal: bool,
-                   exact: bool, f16_fp32_acc: bool = False):
+                   exact: bool, f16_fp32_acc: bool = False, hot_pass: bool = False):
     if grad.indices.numel() == 0:
         return
     d = _update_desc(table, grad)
     fused = fused_update_path(table)
     # convert(eltype(table), opt.eta): the library rounds eta to the table type itself
-    _sparse_sgd([d], opt.eta, _sgd_flags(fused, nontemporal, False, exact, f16_fp32_acc),
+    _sparse_sgd([d], opt.eta, _sgd_flags(fused, nontemporal, False, exact, f16_fp32_acc,
+                                         hot_pass),
                 table.device, table.dtype)
 
 
 def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
                   f16_fp32_acc: bool = False, num_splits=4, nthreads=None, scratchspaces=None,
-                  telemetry_cb=None, indexers=None):
+                  telemetry_cb=None, indexers=None, hot_pass: bool = False):
     if len(tables) != len(grads):
         raise ArgumentError("tables and grads differ in length")
     if telemetry_cb is not None:
@@ -315,7 +321,7 @@ def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
         return
     dev = tables[0].device
     for (fused, dtype), descs in groups.items():
-        flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc)
+        flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc, hot_pass)
         for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
             _sparse_sgd(descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH], opt.eta, flags, dev, dtype)
 
@@ -358,7 +364,7 @@ class PhasedUpdate:
     indexers)`` with the same ``exact`` / ``nontemporal`` / ``f16_fp32_acc``."""
 
     def __init__(self, tables, grads, *, nontemporal: bool = True, exact: bool = False,
-                 f16_fp32_acc: bool = False):
+                 f16_fp32_acc: bool = False, hot_pass: bool = False):
         tables, grads = list(tables), list(grads)
         if len(tables) != len(grads):
             raise ArgumentError("tables and grads differ in length")
@@ -372,7 +378,7 @@ class PhasedUpdate:
         self._calls = []  # (dtype, desc array, n, flags, workspace)
         L = _lib.load()
         for (fused, dtype), descs in groups.items():
-            flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc)
+            flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc, hot_pass)
             for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
                 part = descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH]
                 arr = (_lib.UpdateDesc * len(part))(*part)

@@ -82,6 +82,12 @@ extern "C" {
                                     same descriptors, flags and workspace filled earlier in
                                     stream order ("update all", :216-237); idx is not read
                                     again, so it may be refilled once phase 1 is done */
+#define ET_FLAG_SGD_HOT_PASS 128u /* sparse SGD, non-exact Float32 dim-128 tables with pool
+                                    <= 32: the longest occurrence lists (up to 120 columns
+                                    per table, by a log2 length threshold) are summed
+                                    bag-major over 1024-bag windows instead of by per-
+                                    occurrence gathers (deterministic; EXPERIMENTAL, slower
+                                    today — DESIGN.md §7) */
 
 /* Tables per launch carried in the kernel-argument segment; longer lists are
  * split into several launches by the library. */

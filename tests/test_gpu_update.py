@@ -405,14 +405,14 @@ def test_update_repeated_rows_in_bags(oracle, dim):
         assert bits_equal(host(A.data), ref)
 
 
-@pytest.mark.parametrize("exact", [False, True])
-def test_phased_update_index_overlapping_forward(oracle, exact):
+@pytest.mark.parametrize("exact,hot", [(False, False), (False, True), (True, False)])
+def test_phased_update_index_overlapping_forward(oracle, exact, hot):
     """PhasedUpdate: the index phase (src/sparseupdate.jl:210-213) runs on a side stream
     while maplookup! runs on the main stream, the update phase (:216-237) after both.
     Bit-identical to the one-call update_ (hot rows split into chunks, a Dynamic table
     on the generic path, a Float64 group), the index arrays may be overwritten once the
     index phase is done, and a second update_ reuses the same index work."""
-    rng = np.random.default_rng(77 + exact)
+    rng = np.random.default_rng(77 + exact + 2 * hot)
     dims, rows, B, P = (128, 64, 40), (2000, 7, 300), 1024, 20
     hs = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
     statics = [True, True, False]
@@ -436,11 +436,11 @@ def test_phased_update_index_overlapping_forward(oracle, exact):
 
     opt = et.Descent(0.05)
     ref_tabs, _, ref_grads = make()
-    et.update_(opt, ref_tabs, ref_grads, None, exact=exact)
-    et.update_(opt, ref_tabs, ref_grads, None, exact=exact)
+    et.update_(opt, ref_tabs, ref_grads, None, exact=exact, hot_pass=hot)
+    et.update_(opt, ref_tabs, ref_grads, None, exact=exact, hot_pass=hot)
 
     tabs, idx, grads = make()
-    pu = et.PhasedUpdate(tabs, grads, exact=exact)
+    pu = et.PhasedUpdate(tabs, grads, exact=exact, hot_pass=hot)
     out = torch.empty((B, sum(dims)), dtype=torch.float32, device=DEV)
     main = torch.cuda.current_stream()
     side = torch.cuda.Stream()
@@ -473,3 +473,72 @@ def test_phased_update_requires_index_phase():
                                  dev(np.ones((4, 2), np.int64)))
     with pytest.raises(et.ArgumentError):
         et.PhasedUpdate([tab], [g]).update_(et.Descent(0.1))
+
+
+def _fp64_update_and_scale(base, delta, I, eta32=0.1):
+    """The exact (fp64) Descent update of one table and its error-bound scale
+    |w| + eta * sum |delta| (see test_update_hot_rows_chunked_vs_exact)."""
+    ncols = base.shape[0]
+    ok = (I >= 1) & (I <= ncols)
+    bags = np.repeat(np.arange(I.shape[0]), I.shape[1]).reshape(I.shape)
+    acc = np.zeros(base.shape, np.float64)
+    np.add.at(acc, I[ok] - 1, delta.astype(np.float64)[bags[ok]])
+    absacc = np.zeros(base.shape, np.float64)
+    np.add.at(absacc, I[ok] - 1, np.abs(delta).astype(np.float64)[bags[ok]])
+    eta = np.float64(np.float32(eta32))
+    return base.astype(np.float64) - eta * acc, np.abs(base.astype(np.float64)) + eta * absacc
+
+
+def test_update_hot_column_pass_multi_table(oracle):
+    """The bag-major hot-column pass (opt-in ET_FLAG_SGD_HOT_PASS) (k_hot_pick / k_sgd_hot / k_hot_combine): several
+    dim-128 tables through a Preallocation-strided gradient, a paged table, a batch that
+    is not a multiple of the 1024-bag window or the 32-bag batch, pool 13 (not a multiple
+    of 4), out-of-range indices, and a table with more multi-chunk columns than hot slots
+    (only the columns above the length threshold go bag-major).  Columns outside the hot
+    set are bit-identical to the reference's serial sum, hot ones within the summation
+    bound, and the result repeats bit for bit."""
+    rng = np.random.default_rng(2024)
+    B, P, D = 5000, 13, 128
+    rows = [3000, 170, 40000]
+    bases = [rng.standard_normal((r, D)).astype(np.float32) for r in rows]
+    I0 = np.minimum(rng.zipf(1.1, (B, P)), rows[0])
+    I0 = (rng.permutation(rows[0]) + 1)[I0 - 1]
+    I1 = rng.integers(1, 151, (B, P))  # 150 columns of ~430 occurrences ...
+    I1[:, :2] = rng.integers(151, 154, (B, 2))  # ... and 3 of ~3300
+    I1[rng.random((B, P)) < 0.3] = rng.integers(151, 171, 1)[0]  # one column of ~19500
+    I2 = np.minimum(rng.zipf(1.3, (B, P)), rows[2])
+    I2[7, 3], I2[99, 0], I2[4999, 12] = 0, rows[2] + 1, -5  # skipped
+    hidx = [I0, I1, I2]
+    ld = 8 + 3 * D
+    delta = rng.standard_normal((B, ld)).astype(np.float32)
+
+    def run():
+        tabs = [et.SimpleEmbedding(dev(bases[0]), et.Static(D)),
+                et.SplitEmbedding(dev(bases[1]), 64),
+                et.SimpleEmbedding(dev(bases[2]), et.Static(D))]
+        dd = dev(delta)
+        grads = [et.SparseEmbeddingUpdate(t.lookup_type, dd[:, 8 + k * D:8 + (k + 1) * D],
+                                          dev(i)) for k, (t, i) in enumerate(zip(tabs, hidx))]
+        et.update_(et.Descent(0.1), tabs, grads, None, hot_pass=True)
+        return [host(t.to_dense() if isinstance(t, et.SplitEmbedding) else t.data)
+                for t in tabs]
+
+    out = run()
+    assert all(bits_equal(a, b) for a, b in zip(out, run()))
+    # the oracle gets the skipped entries redirected to an unused column, left out below
+    spare = int(np.flatnonzero(np.bincount(np.clip(I2, 0, rows[2]).ravel(),
+                                           minlength=rows[2] + 1)[1:] == 0)[0]) + 1
+    oidx = [I0, I1, np.where((I2 >= 1) & (I2 <= rows[2]), I2, spare)]
+    assert bits_equal(out[2][spare - 1], bases[2][spare - 1])
+    for k in range(3):
+        ref = bases[k].copy()
+        oracle.sgd(ref, np.ascontiguousarray(delta[:, 8 + k * D:8 + (k + 1) * D]), oidx[k],
+                   0.1, fused=True)
+        counts = np.bincount(oidx[k].ravel(), minlength=rows[k] + 1)
+        short = counts[1:] <= 512
+        if k == 2:
+            short[spare - 1] = False
+        assert bits_equal(out[k][short], ref[short]), f"table {k}: short columns"
+        exact_upd, scale = _fp64_update_and_scale(bases[k], delta[:, 8 + k * D:8 + (k + 1) * D],
+                                                  hidx[k])
+        assert np.all(np.abs(out[k].astype(np.float64) - exact_upd) <= 1e-6 * scale), k
