@@ -93,3 +93,35 @@ def test_argument_errors_need_no_gpu():
     # too many tables for one update call
     big = (_lib.UpdateDesc * 33)()
     assert L.et_sgd_workspace_size(ctypes.addressof(big), 33, ctypes.byref(nb)) == -1
+
+
+def test_phase_flags_need_no_gpu():
+    """ET_FLAG_SGD_INDEX_ONLY / APPLY_ONLY are exclusive; INDEX_ONLY accepts NULL
+    gradients (it never reads them) but still validates the index arrays; the workspace
+    grows by the hot-column region only for dim-128, pool <= 32 tables."""
+    from embtab import _lib
+
+    L = _lib.load()
+    d = (_lib.UpdateDesc * 1)()
+    d[0] = _lib.UpdateDesc(1 << 20, 128, 1000, 128, 20, 0, 128, 1 << 20, 20, 4096)
+    both = _lib.ET_FLAG_SGD_INDEX_ONLY | _lib.ET_FLAG_SGD_APPLY_ONLY
+    assert L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(d), 1, 0.1, both, None, 0, None) == -1
+    assert b"INDEX_ONLY" in L.et_last_error()
+    # delta NULL: an argument error for a full call, not for the index phase (which then
+    # stops at the missing workspace, before any device work)
+    assert L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(d), 1, 0.1, 0, None, 0, None) == -1
+    rc = L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(d), 1, 0.1, _lib.ET_FLAG_SGD_INDEX_ONLY,
+                         None, 0, None)
+    assert rc == -3 and b"workspace" in L.et_last_error()
+    d[0].idx = 0
+    rc = L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(d), 1, 0.1, _lib.ET_FLAG_SGD_INDEX_ONLY,
+                         None, 0, None)
+    assert rc == -1
+    sizes = []
+    for dim, pool in ((128, 20), (64, 20), (128, 40)):
+        d[0] = _lib.UpdateDesc(1 << 20, dim, 1000, dim, pool, 1 << 20, dim, 1 << 20, pool, 4096)
+        nb = ctypes.c_int64(0)
+        assert L.et_sgd_workspace_size(ctypes.addressof(d), 1, ctypes.byref(nb)) == 0
+        sizes.append(nb.value)
+    # the dim-128 pool-20 table carries 120 slots x 4 windows x 512 B of window partials
+    assert sizes[0] > 120 * 4 * 512 + 20 * 4096 * 16
