@@ -311,7 +311,7 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
     # segments, chunk records — it reads only the indices) on a second stream beside the
     # forward lookup; the update phase (:216-237) follows both.
     pu = et.PhasedUpdate(tables, grads)
-    side = torch.cuda.Stream(device)
+    side = torch.cuda.Stream(device, priority=-1)  # high priority: 4.78 vs 4.88 ms (normal)
 
     def step_overlap():
         side.wait_stream(stream)
