@@ -34,6 +34,7 @@ CRITEO_KAGGLE_ROWS = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 9314
                       286181, 105, 142572]
 DIM, POOL, BATCH = 128, 20, 65536
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HBM_COPY_GBS = 6290.0  # measured float4-copy ceiling (MI355X_MICROARCH.md:36), SURVEY.md §8d
 TABLE_SEED, INDEX_SEED = 1000, 2000
 
 
@@ -202,6 +203,7 @@ def bench_config2(et, L, device, steps, warmup):
                       f"{per_launch_ms * 1e3:.2f} us)",
             "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
             "frac_of_hbm_peak": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frac_of_copy_ceiling": nbytes / (ms * 1e-3) / 1e9 / HBM_COPY_GBS,
             "algorithmic_bytes_per_launch": nbytes, "bit_identical": ok}
 
 
@@ -512,6 +514,9 @@ def main():
             "traffic_GBs": (traffic_bytes / (kernel_ms * 1e-3) / 1e9) if traffic_bytes else None,
             "traffic_frac": (traffic_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                              if traffic_bytes else None),
+            # the same fabric rate against the measured float4-copy ceiling (6.29 TB/s)
+            "traffic_frac_of_copy_ceiling": (traffic_bytes / (kernel_ms * 1e-3) / 1e9 /
+                                             HBM_COPY_GBS if traffic_bytes else None),
             "algorithmic_bytes_per_launch": local_bytes,
             "kernel_ms": kernel_ms,
             "kernel_ms_median": kernel_ms_median,
