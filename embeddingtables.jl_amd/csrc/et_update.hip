@@ -1036,11 +1036,7 @@ template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
                      const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl) {
-    static const unsigned grid = [] {
-        const char* e = getenv("ET_SGD_GRID");  // experiments: workgroups of the SGD passes
-        return e ? (unsigned)atoi(e) : 256u * 16u;
-    }();
+                     const HotList& hl, unsigned grid) {
     if constexpr (__is_same(T, float)) {
         if (hl.n > 0 && w.hot_part) {
             hipLaunchKernelGGL(k_sgd_hot, dim3((unsigned)w.hot_nw, (unsigned)hl.n), dim3(256), 0, s,
@@ -1109,10 +1105,10 @@ template <typename T, typename C>
 int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, double eta_c, double eta64,
                      int mode, bool nt, const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl) {
+                     const HotList& hl, unsigned grid) {
 #define ET_SGD_CALL(M, NTV)                                                                \
     return launch_sgd_typed<T, C, M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, (C)eta_c, \
-                                          eta64, vg, any_generic, s, hl)
+                                          eta64, vg, any_generic, s, hl, grid)
     if (mode == 0) {
         if (nt) ET_SGD_CALL(0, true);
         ET_SGD_CALL(0, false);
@@ -1123,6 +1119,19 @@ int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     if (nt) ET_SGD_CALL(2, true);
     ET_SGD_CALL(2, false);
 #undef ET_SGD_CALL
+}
+
+// Workgroups of the chunk / combine passes (grid-stride): one per 2048 occurrences,
+// 256..16384 — 16384 measured 3% faster than 4096 on the config-4 batch (3.72 vs 3.84
+// ms), and small batches launch fewer idle workgroups.
+inline unsigned sgd_grid(int64_t n) {
+    static const int forced = [] {
+        const char* e = getenv("ET_SGD_GRID");  // experiments: a fixed grid
+        return e ? atoi(e) : 0;
+    }();
+    if (forced > 0) return (unsigned)forced;
+    const int64_t g = cdiv64(n, 2048);
+    return (unsigned)(g < 256 ? 256 : g > 16384 ? 16384 : g);
 }
 
 // Tables the hot-column pass can take (the workspace is sized for all of them).
@@ -1282,27 +1291,28 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
     const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;
     const double eta_c = et::convert_eta(dtype, eta);
+    const unsigned grid = et::sgd_grid(n);
     switch (dtype) {
         case ET_F32:
             return et::launch_sgd_dtype<float, float>(pack, ntables, gr, w, chunk, pdim, sent,
                                                       eta_c, eta, mode, nt, vg,
-                                                      any_generic, s, hl);
+                                                      any_generic, s, hl, grid);
         case ET_F64:
             return et::launch_sgd_dtype<double, double>(pack, ntables, gr, w, chunk, pdim, sent,
                                                          eta_c, eta, mode, nt, vg,
-                                                         any_generic, s, hl);
+                                                         any_generic, s, hl, grid);
         case ET_BF16:
             return et::launch_sgd_dtype<__bf16, float>(pack, ntables, gr, w, chunk, pdim, sent,
                                                        eta_c, eta, mode, nt, vg,
-                                                       any_generic, s, hl);
+                                                       any_generic, s, hl, grid);
         default:  // ET_F16
             if (flags & ET_FLAG_F16_FP32_ACC)
                 return et::launch_sgd_dtype<_Float16, float>(pack, ntables, gr, w, chunk, pdim,
                                                              sent, eta_c, eta, mode, nt, vg,
-                                                             any_generic, s, hl);
+                                                             any_generic, s, hl, grid);
             return et::launch_sgd_dtype<_Float16, _Float16>(pack, ntables, gr, w, chunk, pdim,
                                                             sent, eta_c, eta, mode, nt, vg,
-                                                            any_generic, s, hl);
+                                                            any_generic, s, hl, grid);
     }
 }
 
