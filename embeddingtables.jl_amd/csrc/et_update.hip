@@ -30,7 +30,7 @@
 
 namespace et {
 
-constexpr uint32_t kChunk = 512;  // occurrences per chunk (non-exact mode)
+constexpr uint32_t kChunk = ET_SGD_CHUNK;  // occurrences per chunk (non-exact mode)
 
 struct UpdatePack {
     et_update_desc d[ET_MAX_TABLES_PER_LAUNCH];
@@ -454,9 +454,10 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
 }
 
 // Combine pass: every multi-chunk segment (from the appended list, one per workgroup
-// at a time) is reduced by a whole workgroup.  Its
-// partial rows are split into NG = 4*GPW contiguous ranges in chunk order; group G sums
-// range G sequentially (U rows in flight), the NG sums are added in group order
+// at a time) is reduced by a whole workgroup.  Its partial rows are split into NR = 8
+// contiguous ranges in chunk order, whatever the dim (so a feature slice of a table —
+// a shard's piece — combines exactly like the whole table); lane group G sums ranges G,
+// G + NG, ... sequentially (U rows in flight), the NR sums are added in range order
 // through LDS and group 0 applies the update.  Fixed partition => deterministic.
 template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_combine(
@@ -469,9 +470,10 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
     constexpr int GPW = 64 / LPR;
-    constexpr int NG = 4 * GPW;
+    constexpr int NG = 4 * GPW;  // lane groups per workgroup (4..64)
+    constexpr int NR = 8;        // ranges of partials, independent of the dim
     constexpr int U = NV >= 8 ? 1 : 8 / NV;
-    __shared__ u32x4 red[NG][LPR * NV];
+    __shared__ u32x4 red[NR][LPR * NV];
     const int lane = threadIdx.x & 63;
     const int G = threadIdx.x / LPR, sub = lane % LPR;
     const uint32_t M = counters[kCntM];
@@ -488,8 +490,9 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
             const int vpr = pack.d[table_of_key(pack, ntables, keys[seg_start[seg]])].dim / 4;
             int vix[NV];
             vec_index<LPR, NV>(sub, vpr, vix);
-            const uint32_t a = p0 + (uint32_t)((uint64_t)np * G / NG);
-            const uint32_t b = p0 + (uint32_t)((uint64_t)np * (G + 1) / NG);
+            for (int R = G; R < NR; R += NG) {
+            const uint32_t a = p0 + (uint32_t)((uint64_t)np * R / NR);
+            const uint32_t b = p0 + (uint32_t)((uint64_t)np * (R + 1) / NR);
             float acc[NV][4];
 #pragma unroll
             for (int v = 0; v < NV; ++v) acc[v][0] = acc[v][1] = acc[v][2] = acc[v][3] = 0.0f;
@@ -517,14 +520,15 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
             }
 #pragma unroll
             for (int v = 0; v < NV; ++v)
-                red[G][v * LPR + sub] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
+                red[R][v * LPR + sub] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
                                               __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
+            }
             __syncthreads();
             if (G == 0) {
                 float tot[NV][4];
 #pragma unroll
                 for (int v = 0; v < NV; ++v) tot[v][0] = tot[v][1] = tot[v][2] = tot[v][3] = 0.0f;
-                for (int gg = 0; gg < NG; ++gg) {
+                for (int gg = 0; gg < NR; ++gg) {
 #pragma unroll
                     for (int v = 0; v < NV; ++v) {
                         const u32x4 r = red[gg][v * LPR + sub];

@@ -24,6 +24,7 @@ ET_FLAG_SGD_INDEX_ONLY = 32
 ET_FLAG_SGD_APPLY_ONLY = 64
 ET_FLAG_SGD_HOT_PASS = 128
 ET_MAX_TABLES_PER_LAUNCH = 32
+ET_SGD_CHUNK = 256  # include/embtab.h: occurrences per chunk of the non-exact SGD
 ET_ABI_VERSION = 5
 ET_MAX_PEERS = 16
 

@@ -268,7 +268,7 @@ def update_(*args, nontemporal: bool | None = None, exact: bool = False,
 
     ``exact=True`` sums every column's gradient serially (bit-identical to the
     reference even for hot columns); the default splits occurrence lists longer than
-    512 into partial sums combined in a fixed order (deterministic).  Float16 tables
+    ET_SGD_CHUNK (256) into partial sums combined in a fixed order (deterministic).  Float16 tables
     use Julia's Float16 arithmetic unless ``f16_fp32_acc`` (sums in Float32).
     ``hot_pass=True`` (experimental, ET_FLAG_SGD_HOT_PASS) sums the longest occurrence
     lists of Float32 dim-128 tables bag-major (deterministic, not bit-identical to the

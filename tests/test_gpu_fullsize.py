@@ -146,7 +146,7 @@ def test_config4_full_size(oracle, criteo):
             oracle.sgd(w, dsub, np.ones(len(bags), np.int64), 0.1, fused=True)
             got = A.data[c].cpu().numpy()
             n = len(bags)
-            if n <= 512:   # one chunk: the serial sum, bit-identical
+            if n <= et._lib.ET_SGD_CHUNK:   # one chunk: the serial sum, bit-identical
                 assert w[0].tobytes() == got.tobytes(), (t, c, n)
             else:
                 # chunked: against the EXACT update, 1e-6 of |w| + eta * sum|delta| (the

@@ -92,7 +92,7 @@ def test_split_update_vs_oracle(oracle, dim, cps, exact):
     et.update_(et.Descent(0.5), A, g, exact=exact)
     ref = base.copy()
     oracle.sgd(ref, delta, I, 0.5, fused=fused_update_path(A))
-    assert bits_equal(host(A.to_dense()), ref)  # no column has > 512 occurrences here
+    assert bits_equal(host(A.to_dense()), ref)  # no column has > ET_SGD_CHUNK occurrences here
 
 
 def test_split_update_dynamic_and_indexer_view(oracle):

@@ -11,6 +11,7 @@ import embtab as et
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
+CHUNK = et._lib.ET_SGD_CHUNK  # occurrences per chunk of the non-exact update
 
 
 def dev(x):
@@ -90,7 +91,7 @@ def test_update_exact_vs_oracle(oracle, dim, static, reducing):
 
 
 def test_update_hot_rows_chunked_vs_exact(oracle):
-    """Zipf-skewed indices: occurrence lists longer than the 512-entry chunk are summed
+    """Zipf-skewed indices: occurrence lists longer than the ET_SGD_CHUNK-entry chunk are summed
     as ordered partial sums (deterministic) — within 1e-6 rel of the serial sum; the
     exact mode is bit-identical."""
     rng = np.random.default_rng(12)
@@ -103,7 +104,7 @@ def test_update_hot_rows_chunked_vs_exact(oracle):
     ref = base.copy()
     oracle.sgd(ref, delta, I, 0.1, fused=True)
     counts = np.bincount(I.ravel(), minlength=ncols + 1)
-    assert counts.max() > 4 * 512  # the test really has split rows
+    assert counts.max() > 4 * CHUNK  # the test really has split rows
     res = {}
     for exact in (True, False):
         A = et.SimpleEmbedding(dev(base), et.Static(dim))
@@ -111,7 +112,7 @@ def test_update_hot_rows_chunked_vs_exact(oracle):
                                                                 dev(I)), exact=exact)
         res[exact] = host(A.data)
     assert bits_equal(res[True], ref)
-    hot = counts[1:] > 512
+    hot = counts[1:] > CHUNK
     assert bits_equal(res[False][~hot], ref[~hot])
     # Tolerance for the reassociated hot-column sums, measured against the EXACT (fp64)
     # update: 1e-6 relative to the magnitude of the computation's inputs,
@@ -244,7 +245,7 @@ def test_update_typed_vs_oracle(oracle, kind, dim, static, exact):
     base = _typed(rng, (ncols, dim), kind)
     delta = _typed(rng, (B, dim), kind)
     I = rng.integers(1, ncols + 1, (B, P))
-    I[:, 0] = 7  # one column with 256 occurrences, another with > 512 (partials)
+    I[:, 0] = 7  # one column with ~256 occurrences, another with 768 (partials)
     I[:, 1:4] = 11
     A = et.SimpleEmbedding(_dev_typed(base, kind), et.Static(dim) if static else et.Dynamic)
     from embtab.tables import fused_update_path
@@ -255,8 +256,10 @@ def test_update_typed_vs_oracle(oracle, kind, dim, static, exact):
     oracle.sgd(ref, delta, I, 0.1, fused=fused_update_path(A), bf16=kind == "bf16",
                f16_fp32_acc=kind == "f16acc")
     got = _host_bits(A.data)
-    hot = np.zeros(ncols, bool)
-    hot[10] = True  # column 11: 768 occurrences, summed as ordered partials unless exact
+    # columns with more than ET_SGD_CHUNK occurrences (11: 768; 7: 256 + its random
+    # ones) are summed as ordered partials unless exact
+    hot = np.bincount(I.ravel(), minlength=ncols + 1)[1:] > CHUNK
+    assert hot[10]
     if exact:
         assert bits_equal(got, ref.view(got.dtype))
     else:
@@ -356,7 +359,7 @@ def test_forward_and_update_capture_in_a_hip_graph(oracle):
 def test_update_masked_vector_dims(oracle, dim):
     """Float32 tables of any dim that is a multiple of 4 run the vector SGD kernels at
     the next power-of-two capacity (masked): exact mode bit-identical to the oracle,
-    chunked mode bit-identical on every column with <= 512 occurrences."""
+    chunked mode bit-identical on every column with <= ET_SGD_CHUNK occurrences."""
     rng = np.random.default_rng(dim)
     ncols, B, P = 400, 300, 6
     base = rng.standard_normal((ncols, dim)).astype(np.float32)
@@ -535,7 +538,7 @@ def test_update_hot_column_pass_multi_table(oracle):
         oracle.sgd(ref, np.ascontiguousarray(delta[:, 8 + k * D:8 + (k + 1) * D]), oidx[k],
                    0.1, fused=True)
         counts = np.bincount(oidx[k].ravel(), minlength=rows[k] + 1)
-        short = counts[1:] <= 512
+        short = counts[1:] <= CHUNK
         if k == 2:
             short[spare - 1] = False
         assert bits_equal(out[k][short], ref[short]), f"table {k}: short columns"
