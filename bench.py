@@ -38,10 +38,45 @@ HBM_COPY_GBS = 6290.0  # measured float4-copy ceiling (MI355X_MICROARCH.md:36), 
 TABLE_SEED, INDEX_SEED = 1000, 2000
 
 
+INFINITY_CACHE = 256 << 20  # MI355X die-level L3 (MI355X_MICROARCH.md, Infinity Cache)
+
+
 def algorithmic_bytes(batch, pool, dims, es=4):
     """Per launch: every gathered row + every index + every output element
     (SURVEY.md §8d), summed over the tables (or table pieces) of the launch."""
     return sum(batch * pool * d * es + batch * pool * 8 + batch * d * es for d in dims)
+
+
+def hbm_compulsory_bytes(batch, pool, dims, rows, es=4):
+    """Per launch, the bytes that MUST come from HBM whatever the caches hold: the
+    gathered rows of every table (piece) larger than the 256 MiB Infinity Cache (a
+    smaller one can stay on die from one launch to the next), every index and every
+    output element.  A lower bound on the launch's DRAM bytes, so bytes / time / 8 TB/s
+    is a lower bound on the HBM fraction (<= 1 by construction)."""
+    tot = 0
+    for d, R in zip(dims, rows):
+        tot += batch * pool * 8 + batch * d * es
+        if R * d * es > INFINITY_CACHE:
+            tot += batch * pool * d * es
+    return tot
+
+
+def host_cpus():
+    """(host cores, CPUs this process may run on, cgroup CPU quota or None)."""
+    cores = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = cores
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return cores, usable, quota
 
 
 def parse():
@@ -52,14 +87,16 @@ def parse():
     p.add_argument("--batch", type=int, default=BATCH)
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="target CPU-baseline sample duration (0 disables)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or 16")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU-baseline threads; 0 = every host core (os.cpu_count())")
     p.add_argument("--no-check", action="store_true", help="skip the CPU/GPU bit comparison")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the config-2 (gather) and config-4 (Zipf + SGD) measurements")
     p.add_argument("--force-shard", action="store_true",
                    help="use the sharded (all-gather + concat) step even on one rank")
-    p.add_argument("--plan", choices=["featurewise", "tablewise"], default="featurewise",
-                   help="N > 1: equal feature ranges (default) or whole tables per rank")
+    p.add_argument("--plan", choices=["featurewise", "tablewise"], default="tablewise",
+                   help="N > 1: whole tables per rank, balanced by count (default, SURVEY.md "
+                        "§8e), or equal feature ranges cut at 32-feature granules")
     p.add_argument("--chunks", type=int, default=4,
                    help="N > 1: batch chunks pipelined through lookup / all-gather / concat")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -136,10 +173,16 @@ def cpu_baseline(gpu_out, idx, batch, seconds, threads, check):
         if el >= seconds or steps >= 1000:
             break
     lookups = steps * batch * len(tabs) * POOL
+    cores, usable, quota = host_cpus()
     return {
         "value": lookups / el,
         "unit": "lookups/s",
         "cores": threads,
+        "threads": threads,
+        "host_cores": cores,
+        "cpus_usable": usable,  # sched_getaffinity of this process
+        "cgroup_cpu_quota": quota,  # cpu.max of this process's cgroup (None = no limit)
+        "isa": "gcc -O3 -march=x86-64-v4 (AVX-512)",
         "kind": "port",
         "sample": f"{steps} full step(s) of the same workload ({batch} bags x {len(tabs)} tables "
                   f"x pool {POOL}, same tables and indices) in {el:.2f} s; C restatement of "
@@ -168,9 +211,15 @@ def _timed(fn, steps, warmup, stream):
     return sum(a.elapsed_time(b) for a, b in ev) / steps
 
 
-def bench_config2(et, L, device, steps, warmup):
+def bench_config2(et, L, device, steps, warmup, nsets=16):
     """BASELINE configs[1]: one 128 x 1e7 fp32 table, vector-index (non-reducing) gather,
-    B = 65536.  Bytes per lookup: 512 read + 512 written + 8 index."""
+    B = 65536.  Bytes per lookup: 512 read + 512 written + 8 index.
+
+    Cold-cache method: `nsets` independent index sets (different seeds) are rotated over
+    the back-to-back launches, so consecutive uses of one set are nsets - 1 launches
+    apart; between them nsets x (33.5 MB of rows + 33.5 MB of output) = 1.07 GB pass
+    through the die, 4x the 256 MiB Infinity Cache, so no launch finds its rows on die
+    (a single repeated set — the round-1 method — measured the Infinity Cache instead)."""
     import torch
     from embtab import _lib
 
@@ -179,31 +228,48 @@ def bench_config2(et, L, device, steps, warmup):
     data = torch.empty((R, DIM), dtype=torch.float32, device=device)
     _lib.check(L.et_fill_uniform(_lib.ET_F32, data.data_ptr(), data.numel(), 3000, 0, 0.0, 1.0,
                                  stream.cuda_stream))
-    I = torch.empty(B, dtype=torch.int64, device=device)
-    _lib.check(L.et_fill_index_uniform(I.data_ptr(), B, R, 3001, 0, stream.cuda_stream))
+    sets = []
+    for k in range(nsets):
+        I = torch.empty(B, dtype=torch.int64, device=device)
+        _lib.check(L.et_fill_index_uniform(I.data_ptr(), B, R, 3001 + k, 0, stream.cuda_stream))
+        sets.append(I)
     A = et.SimpleEmbedding(data, et.Static(DIM))
-    dst = torch.empty((B, DIM), dtype=torch.float32, device=device)
-    per_launch_ms = _timed(lambda: et.lookup_(dst, A, I), steps, warmup, stream)
+    dsts = [torch.empty((B, DIM), dtype=torch.float32, device=device) for _ in range(nsets)]
+
+    def run(n, rotate=True):
+        for k in range(n):
+            j = k % nsets if rotate else 0
+            et.lookup_(dsts[j], A, sets[j])
+
+    run(warmup * nsets)
     # a ~12 us launch is timed over back-to-back launches (one event
     # pair around all of them), so the per-launch event overhead does not count
+    n = max(steps, nsets) // nsets * nsets
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    a.record(stream)
-    for _ in range(steps):
-        et.lookup_(dst, A, I)
-    b.record(stream)
-    torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / steps
-    ok = bool(torch.equal(dst, data[I - 1]))  # bit copy check (torch gather as checker)
+
+    def timed(rotate):
+        torch.cuda.synchronize()
+        a.record(stream)
+        run(n, rotate)
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / n
+
+    ms = timed(True)
+    warm_ms = timed(False)  # one repeated set: the Infinity-Cache rate, for reference only
+    ok = all(bool(torch.equal(dsts[j], data[sets[j] - 1])) for j in range(nsets))  # bit copy
     nbytes = B * (DIM * 4 * 2 + 8)
-    del data
+    del data, dsts
     return {"workload": "1 table 128 x 1e7 fp32, vector-index gather, B=65536",
             "lookups_per_s": B / (ms * 1e-3), "kernel_ms": ms,
-            "timing": f"{steps} back-to-back launches (per-launch event pairs: "
-                      f"{per_launch_ms * 1e3:.2f} us)",
+            "timing": f"{n} back-to-back launches, one event pair around them",
+            "cold_cache_method": f"{nsets} independent index sets rotated over the launches "
+                                 f"({nsets} x 67 MB of rows + output between two uses of a "
+                                 "set, 4x the 256 MiB Infinity Cache)",
             "achieved_GBs": nbytes / (ms * 1e-3) / 1e9,
             "frac_of_hbm_peak": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "frac_of_copy_ceiling": nbytes / (ms * 1e-3) / 1e9 / HBM_COPY_GBS,
+            "warm_repeated_set_kernel_ms": warm_ms,
             "algorithmic_bytes_per_launch": nbytes, "bit_identical": ok}
 
 
@@ -461,7 +527,11 @@ def main():
     lookups_per_step = B * T * POOL
     value = lookups_per_step * args.steps / elapsed
     local_bytes = algorithmic_bytes(B, POOL, local_dims)
-    achieved = local_bytes / (kernel_ms * 1e-3) / 1e9
+    local_rows = ([CRITEO_KAGGLE_ROWS[p.table] for p in pieces] if sharded
+                  else [CRITEO_KAGGLE_ROWS[t] for t in mine])
+    hbm_bytes = hbm_compulsory_bytes(B, POOL, local_dims, local_rows)
+    achieved = hbm_bytes / (kernel_ms * 1e-3) / 1e9
+    algorithmic_GBs = local_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = load_traffic()
     traffic_bytes = None
     if traffic and traffic.get("workload") == f"criteo26_b{B}" and world == 1:
@@ -491,9 +561,10 @@ def main():
             "dim": DIM,
             "table_rows": CRITEO_KAGGLE_ROWS,
             "parallelism": "single GPU" if not sharded else
-                           ("table-wise, balanced: contiguous table ranges per GPU, boundary "
-                            "tables cut at 32-feature granularity" if args.plan == "featurewise"
-                            else "table-wise: whole tables per GPU")
+                           ("feature-wise: equal contiguous feature ranges per GPU, tables "
+                            "cut at 32-feature granules" if args.plan == "featurewise"
+                            else "table-wise: whole tables per GPU, contiguous groups balanced "
+                                 "by count (SURVEY.md §8e)")
                            + f" x{world} + "
                            f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-gather concat "
                            f"({shard.chunks} pipelined batch chunks)",
@@ -503,10 +574,18 @@ def main():
         "roofline": {
             "bound": "hbm",
             "kernel": "k_pooled_vec_striped<float,float,128,8,NT,0,SG=1> (scalar-addressed)",
+            # achieved = HBM-compulsory bytes (rows of the tables larger than the 256 MiB
+            # Infinity Cache + all indices + the output) / average launch time: a lower
+            # bound on the DRAM rate, so frac <= 1; the cache-inclusive SURVEY.md §8d
+            # figure is algorithmic_GBs / algorithmic_frac below
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
+            "bytes_basis": "HBM-compulsory: gathered rows of tables > 256 MiB + indices + output",
+            "hbm_compulsory_bytes_per_launch": hbm_bytes,
+            "algorithmic_GBs": algorithmic_GBs,
+            "algorithmic_frac": algorithmic_GBs / HBM_PEAK_GBS,
             "traffic": traffic_bytes,
             # fabric-side bytes (PMC, per launch) over the same launch time: how close the
             # memory system itself runs to the HBM peak (cache-resident tables make the
@@ -546,11 +625,10 @@ def main():
                                        "lookups_per_s": lookups_per_step / (ms16 * 1e-3)}
         del dst16
     if world == 1 and not args.no_extra:
-        result["config2_gather"] = bench_config2(et, L, device, 200, 10)
+        result["config2_gather"] = bench_config2(et, L, device, 320, 2)
         result["config4_zipf_update"] = bench_config4(et, tables, mine, device, 10, 2, B)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 16)
-        threads = max(1, min(threads, os.cpu_count() or 1))
+        threads = args.cpu_threads or (os.cpu_count() or 1)
         gpu_out = None if args.no_check else dst.cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(gpu_out, idx, B, args.cpu_seconds, threads,
                                               not args.no_check)
