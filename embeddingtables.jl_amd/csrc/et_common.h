@@ -66,8 +66,28 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 // Device-side helpers
 // ---------------------------------------------------------------------------
 
-// Out-of-range index counter (read + cleared by et_check_errors).
-__device__ unsigned long long g_oob_count;
+// Out-of-range index counter, one per translation unit (internal linkage, so the
+// kernels of each TU need no relocatable device code); each TU exports its reader
+// through ET_OOB_READER and et_check_errors sums them.
+static __device__ unsigned long long g_oob_count;
+
+int oob_take_lookup(uint64_t* v);
+int oob_take_update(uint64_t* v);
+int oob_take_misc(uint64_t* v);
+
+// Read and clear this TU's counter (the device is synchronised by the caller).
+#define ET_OOB_READER(name)                                                              \
+    namespace et {                                                                       \
+    int oob_take_##name(uint64_t* v) {                                                   \
+        unsigned long long x = 0, zero = 0;                                              \
+        ET_HIP_CHECK(hipMemcpyFromSymbol(&x, HIP_SYMBOL(g_oob_count), sizeof(x), 0,      \
+                                         hipMemcpyDeviceToHost));                        \
+        ET_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_oob_count), &zero, sizeof(zero), 0,  \
+                                       hipMemcpyHostToDevice));                          \
+        *v = x;                                                                          \
+        return ET_OK;                                                                    \
+    }                                                                                    \
+    }
 
 __device__ __forceinline__ void note_oob(int n = 1) { atomicAdd(&g_oob_count, (unsigned long long)n); }
 
@@ -99,6 +119,36 @@ __host__ __device__ __forceinline__ uint64_t hash64(uint64_t z) {
 
 __host__ __device__ __forceinline__ uint64_t fill_hash(uint64_t seed, uint64_t i) {
     return hash64(seed * 0xD1B54A32D192ED03ull + i);
+}
+
+// ---------------------------------------------------------------------------
+// Shared by the lookup and update translation units
+// ---------------------------------------------------------------------------
+// Address of column `row` (0-based) of a contiguous or paged (SplitEmbedding) table.
+template <typename T>
+__device__ __forceinline__ T* col_ptr(const void* table, int64_t ld, int64_t cols_per_page,
+                                      uint64_t row) {
+    if (cols_per_page > 0) {
+        T* const* pages = reinterpret_cast<T* const*>(table);
+        return pages[row / (uint64_t)cols_per_page] + (row % (uint64_t)cols_per_page) * ld;
+    }
+    return (T*)table + row * (uint64_t)ld;
+}
+
+constexpr int kVecDims[] = {16, 32, 64, 128, 256, 512};
+
+inline bool vec_dim_ok(int D) {
+    for (int x : kVecDims)
+        if (x == D) return true;
+    return false;
+}
+
+// Dims that are a multiple of 16 bytes but not a power-of-two vector width: the masked
+// vector kernel at the next power-of-two capacity (up to 2048 elements).
+inline int masked_capacity(int D) {
+    int c = 16;
+    while (c < D) c <<= 1;
+    return c;
 }
 
 }  // namespace et

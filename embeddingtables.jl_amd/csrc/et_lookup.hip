@@ -574,17 +574,6 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
     }
 }
 
-// Address of column `row` (0-based) of a contiguous or paged (SplitEmbedding) table.
-template <typename T>
-__device__ __forceinline__ T* col_ptr(const void* table, int64_t ld, int64_t cols_per_page,
-                                      uint64_t row) {
-    if (cols_per_page > 0) {
-        T* const* pages = reinterpret_cast<T* const*>(table);
-        return pages[row / (uint64_t)cols_per_page] + (row % (uint64_t)cols_per_page) * ld;
-    }
-    return (T*)table + row * (uint64_t)ld;
-}
-
 // Generic path: any feature size / alignment / per-table dims / paged tables.  One wave
 // per bag, lanes stride over the features, pool order sequential per feature.
 // Store conversion T -> O; bfloat16 converts through float (exact for 16-bit types).
@@ -645,14 +634,6 @@ __global__ __launch_bounds__(256) void k_pooled_generic(LookupPack pack, int nta
 // ---------------------------------------------------------------------------
 // Host dispatch
 // ---------------------------------------------------------------------------
-
-constexpr int kVecDims[] = {16, 32, 64, 128, 256, 512};
-
-inline bool vec_dim_ok(int D) {
-    for (int x : kVecDims)
-        if (x == D) return true;
-    return false;
-}
 
 inline bool gather_rb_ok(int64_t rb) {
     return rb == 32 || rb == 64 || rb == 128 || rb == 256 || rb == 512 || rb == 1024 ||
@@ -878,14 +859,6 @@ int launch_pooled_dim(const LookupPack& pack, int n, int D, int64_t batch, void*
         case 512: return launch_pooled_vec<T, A, 512, NT, PG>(pack, n, batch, dst, ld_dst, s);
     }
     return fail(ET_ERR_UNSUPPORTED, "vector dim %d", D);
-}
-
-// Dims that are a multiple of 16 bytes but not a power-of-two vector width: the masked
-// vector kernel at the next power-of-two capacity (up to 2048 elements).
-inline int masked_capacity(int D) {
-    int c = 16;
-    while (c < D) c <<= 1;
-    return c;
 }
 
 template <typename T, typename A, bool NT>
@@ -1193,3 +1166,5 @@ extern "C" int et_maplookup_prealloc_to(int dtype, int dst_dtype, const et_looku
     return et::lookup_dispatch_convert(dtype, dst_dtype, descs, ntables, batch, dst, ld_dst,
                                        flags, s);
 }
+
+ET_OOB_READER(lookup)

@@ -264,14 +264,16 @@ extern "C" int et_split_slabs(int dtype, const void* src, int64_t ld_src, int64_
                                const_cast<void*>(src), ld_src, stream);
 }
 
+ET_OOB_READER(misc)
+
 extern "C" int et_check_errors(uint64_t* oob_count) {
     et::clear_err();
     ET_HIP_CHECK(hipDeviceSynchronize());
-    unsigned long long v = 0, zero = 0;
-    ET_HIP_CHECK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(et::g_oob_count), sizeof(v), 0,
-                                     hipMemcpyDeviceToHost));
-    ET_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(et::g_oob_count), &zero, sizeof(zero), 0,
-                                   hipMemcpyHostToDevice));
-    if (oob_count) *oob_count = v;
+    uint64_t a = 0, b = 0, c = 0;
+    int st;
+    if ((st = et::oob_take_lookup(&a)) != ET_OK) return st;
+    if ((st = et::oob_take_update(&b)) != ET_OK) return st;
+    if ((st = et::oob_take_misc(&c)) != ET_OK) return st;
+    if (oob_count) *oob_count = a + b + c;
     return ET_OK;
 }

@@ -1580,3 +1580,5 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
     }
 #undef ET_UI_T
 }
+
+ET_OOB_READER(update)

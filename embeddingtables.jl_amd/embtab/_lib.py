@@ -25,8 +25,11 @@ ET_FLAG_SGD_APPLY_ONLY = 64
 ET_FLAG_SGD_HOT_PASS = 128
 ET_MAX_TABLES_PER_LAUNCH = 32
 ET_SGD_CHUNK = 256  # include/embtab.h: occurrences per chunk of the non-exact SGD
-ET_ABI_VERSION = 5
+ET_ABI_VERSION = 6
 ET_MAX_PEERS = 16
+ET_PLAN_TABLEWISE, ET_PLAN_FEATUREWISE = 0, 1
+ET_EXCHANGE_ALLGATHER, ET_EXCHANGE_ALLTOALL = 0, 1
+ET_COMM_ID_BYTES = 128
 
 TORCH_TO_ET = {
     torch.float32: ET_F32,
@@ -56,6 +59,16 @@ EXPORTS = (
     "et_ipc_handle",
     "et_ipc_open",
     "et_ipc_close",
+    "et_shard_plan",
+    "et_comm_unique_id",
+    "et_comm_init",
+    "et_comm_destroy",
+    "et_allgather_concat",
+    "et_sharded_create",
+    "et_sharded_info",
+    "et_sharded_maplookup",
+    "et_sharded_piece_grads",
+    "et_sharded_destroy",
     "et_fill_uniform",
     "et_fill_index_uniform",
     "et_check_errors",
@@ -79,6 +92,18 @@ class LookupDesc(ctypes.Structure):
         ("ld_idx", ctypes.c_int64),
         ("dst_row_off", ctypes.c_int64),
         ("cols_per_page", ctypes.c_int64),
+    ]
+
+
+class ShardPiece(ctypes.Structure):
+    """et_shard_piece (include/embtab.h)."""
+
+    _fields_ = [
+        ("rank", ctypes.c_int32),
+        ("table", ctypes.c_int32),
+        ("f0", ctypes.c_int32),
+        ("dim", ctypes.c_int32),
+        ("col", ctypes.c_int64),
     ]
 
 
@@ -135,6 +160,16 @@ def load() -> ctypes.CDLL:
         "et_ipc_handle": ([vp, vp, vp], c_int),
         "et_ipc_open": ([vp, i64, vp], c_int),
         "et_ipc_close": ([vp, i64], c_int),
+        "et_shard_plan": ([i32, i32, vp, vp, i32, i64, i32, i32, vp, i32, vp], c_int),
+        "et_comm_unique_id": ([vp], c_int),
+        "et_comm_init": ([vp, i32, vp, i32], c_int),
+        "et_comm_destroy": ([vp], c_int),
+        "et_allgather_concat": ([vp, c_int, vp, i64, i64, vp, i32, vp, vp, vp, i64, vp], c_int),
+        "et_sharded_create": ([vp, vp, i32, i32, c_int, vp, i32, i64, i64, i64, i32, i32], c_int),
+        "et_sharded_info": ([vp, vp, vp, vp, vp], c_int),
+        "et_sharded_maplookup": ([vp, vp, i32, vp, i64, vp, i64, u32, vp], c_int),
+        "et_sharded_piece_grads": ([vp, vp, i64, vp, vp, i64, vp], c_int),
+        "et_sharded_destroy": ([vp], c_int),
         "et_fill_uniform": ([c_int, vp, i64, u64, u64, dbl, dbl, vp], c_int),
         "et_fill_index_uniform": ([vp, i64, i64, u64, u64, vp], c_int),
         "et_check_errors": ([vp], c_int),

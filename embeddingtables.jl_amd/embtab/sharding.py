@@ -38,33 +38,6 @@ from .lookup import _ld
 VEC_DIMS = (512, 256, 128, 64, 32, 16)  # the vector kernels' feature widths
 
 
-def plan_tables(ntables: int, world: int, sizes=None) -> list[list[int]]:
-    """Balance whole tables over ranks by COUNT (every table costs B*P*D*4 bytes per
-    lookup whatever its cardinality), contiguous groups, the largest tables spread
-    over distinct ranks when ``sizes`` is given (SURVEY.md §8e: 26 tables on 8 GPUs
-    -> 4,4,3,3,3,3,3,3)."""
-    if world <= 0:
-        raise ValueError("world must be positive")
-    base, extra = divmod(ntables, world)
-    counts = [base + (1 if r < extra else 0) for r in range(world)]
-    if sizes is None:
-        out, t = [], 0
-        for c in counts:
-            out.append(list(range(t, t + c)))
-            t += c
-        return out
-    # deal tables in descending size round-robin, respecting the counts
-    order = sorted(range(ntables), key=lambda t: -sizes[t])
-    out = [[] for _ in range(world)]
-    r = 0
-    for t in order:
-        while len(out[r]) >= counts[r]:
-            r = (r + 1) % world
-        out[r].append(t)
-        r = (r + 1) % world
-    return [sorted(o) for o in out]
-
-
 @dataclass(frozen=True)
 class Piece:
     """Features ``[f0, f0 + dim)`` of global table ``table``; its columns of the
@@ -76,41 +49,48 @@ class Piece:
     col: int
 
 
-def _vec_split(t: int, f0: int, dim: int, col: int, es: int = 4) -> list[Piece]:
-    """Cut a feature range into vector-kernel widths where alignment allows (96 ->
-    64 + 32); anything else stays one piece (the generic kernel takes it)."""
-    out = []
-    while dim > 0:
-        w = next((v for v in VEC_DIMS if v <= dim and (f0 * es) % 16 == 0), None)
-        if w is None or (dim not in VEC_DIMS and dim % 16 != 0):
-            out.append(Piece(t, f0, dim, col))
-            break
-        out.append(Piece(t, f0, w, col))
-        f0, dim, col = f0 + w, dim - w, col + w
-    return out
+def native_plan(mode: int, dims, world: int, prependrows: int = 0, sizes=None,
+                granule: int = 32, elsize: int = 4) -> list[list[Piece]]:
+    """et_shard_plan (host-only C++ in the library): every rank's pieces, in slab order."""
+    if world <= 0:
+        raise ValueError("world must be positive")
+    L = _lib.load()
+    n = len(dims)
+    d = (ctypes.c_int32 * max(1, n))(*dims)
+    sz = (ctypes.c_int64 * max(1, n))(*sizes) if sizes is not None else None
+    cnt = ctypes.c_int32(0)
+    args = (mode, n, ctypes.addressof(d), ctypes.addressof(sz) if sz is not None else None,
+            world, prependrows, granule, elsize)
+    _lib.check(L.et_shard_plan(*args, None, 0, ctypes.byref(cnt)))
+    out = (_lib.ShardPiece * max(1, cnt.value))()
+    _lib.check(L.et_shard_plan(*args, ctypes.addressof(out), cnt.value, ctypes.byref(cnt)))
+    pieces = [[] for _ in range(world)]
+    for i in range(cnt.value):
+        p = out[i]
+        pieces[p.rank].append(Piece(p.table, p.f0, p.dim, p.col))
+    return pieces
+
+
+def plan_tables(ntables: int, world: int, sizes=None) -> list[list[int]]:
+    """Whole tables over ranks balanced by COUNT (every table costs B*P*D*4 bytes per
+    lookup whatever its cardinality), contiguous groups, the largest tables spread
+    over distinct ranks when ``sizes`` is given (SURVEY.md §8e: 26 tables on 8 GPUs
+    -> 4,4,3,3,3,3,3,3).  Thin view of et_shard_plan(ET_PLAN_TABLEWISE)."""
+    pieces = native_plan(_lib.ET_PLAN_TABLEWISE, [1] * ntables, world, sizes=sizes)
+    return [[p.table for p in ps] for ps in pieces]
 
 
 def plan_features(dims, world: int, granule: int = 32) -> list[tuple[int, int]]:
-    """Feature ranges ``[lo, hi)`` of the concatenated feature axis, one per rank:
-    cut points are table edges or multiples of ``granule`` inside a table, each
-    chosen nearest to an equal split."""
-    if world <= 0:
-        raise ValueError("world must be positive")
-    cuts, start = {0}, 0
-    for d in dims:
-        for f in range(granule, d, granule):
-            cuts.add(start + f)
-        start += d
-        cuts.add(start)
-    F = start
-    cands = sorted(cuts)
-    bounds = [0]
-    for r in range(1, world):
-        target = F * r / world
-        best = min((c for c in cands if c >= bounds[-1]), key=lambda c: (abs(c - target), c))
-        bounds.append(best)
-    bounds.append(F)
-    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+    """Feature ranges ``[lo, hi)`` of the concatenated feature axis, one per rank (cut
+    points: table edges or multiples of ``granule`` inside a table, each nearest to an
+    equal split).  Thin view of et_shard_plan(ET_PLAN_FEATUREWISE)."""
+    pieces = native_plan(_lib.ET_PLAN_FEATUREWISE, dims, world, granule=granule)
+    out, lo = [], 0
+    for ps in pieces:
+        hi = max((p.col + p.dim for p in ps), default=lo)
+        out.append((lo, hi))
+        lo = hi
+    return out
 
 
 class ShardPlan:
@@ -128,25 +108,14 @@ class ShardPlan:
 
     @classmethod
     def tablewise(cls, dims, world: int, prependrows: int = 0, sizes=None) -> "ShardPlan":
-        offs = _table_cols(dims, prependrows)
-        return cls(dims, prependrows,
-                   [[Piece(t, 0, dims[t], offs[t]) for t in ts]
-                    for ts in plan_tables(len(dims), world, sizes)])
+        return cls(dims, prependrows, native_plan(_lib.ET_PLAN_TABLEWISE, dims, world,
+                                                  prependrows, sizes))
 
     @classmethod
     def featurewise(cls, dims, world: int, prependrows: int = 0,
-                    granule: int = 32) -> "ShardPlan":
-        offs = _table_cols(dims, prependrows)
-        starts = [o - prependrows for o in offs]
-        pieces = []
-        for lo, hi in plan_features(dims, world, granule):
-            mine = []
-            for t, d in enumerate(dims):
-                a, b = max(lo, starts[t]), min(hi, starts[t] + d)
-                if a < b:
-                    mine += _vec_split(t, a - starts[t], b - a, prependrows + a)
-            pieces.append(mine)
-        return cls(dims, prependrows, pieces)
+                    granule: int = 32, elsize: int = 4) -> "ShardPlan":
+        return cls(dims, prependrows, native_plan(_lib.ET_PLAN_FEATUREWISE, dims, world,
+                                                  prependrows, None, granule, elsize))
 
     def tables_of(self, rank: int) -> list[int]:
         """Global ids of the tables rank ``rank`` reads (each once, in order)."""
@@ -186,14 +155,6 @@ class ShardPlan:
         return launches
 
 
-def _table_cols(dims, prependrows):
-    offs, c = [], prependrows
-    for d in dims:
-        offs.append(c)
-        c += d
-    return offs
-
-
 def piece_table(full, piece: Piece):
     """A rank's view of ``piece`` of a full table (a SimpleEmbedding on a column
     slice; whole-table pieces return the table itself).  The view keeps the
@@ -217,7 +178,8 @@ class ShardedMapLookup:
     their index arrays, in ``plan.pieces[rank]`` order."""
 
     def __init__(self, plan: ShardPlan, rank: int, world: int, batch: int, dtype, device,
-                 group=None, exchange: str = "allgather", chunks: int = 1):
+                 group=None, exchange: str = "allgather", chunks: int = 1, native=None,
+                 rccl=None):
         if plan.world != world:
             raise ValueError("plan and world size differ")
         if exchange not in ("allgather", "alltoall", "p2p"):
@@ -225,6 +187,26 @@ class ShardedMapLookup:
         self.plan, self.rank, self.world, self.batch = plan, rank, world, batch
         self.device, self.group, self.exchange_kind = torch.device(device), group, exchange
         self.chunks = max(1, min(chunks, batch)) if exchange != "alltoall" else 1
+        self.dtype = dtype
+        self._native = None
+        if native is None:  # the C-ABI step whenever the ranks are real GPU processes
+            native = (exchange != "p2p" and self.device.type == "cuda" and
+                      (world == 1 or self._nccl_group()))
+        if native:
+            self._native = NativeShardedStep(plan, rank, world, batch, dtype, self.device,
+                                             group, exchange, self.chunks,
+                                             rccl=world > 1 if rccl is None else rccl)
+            self.launches = plan.assembly_launches()
+            nat = self._native
+            # the slab is the head of the native workspace (for lookup-only timing)
+            es = torch.empty((), dtype=dtype).element_size()
+            self.slab = nat.workspace[:batch * nat.slab_ld * es].view(dtype).view(
+                batch, nat.slab_ld)
+            self.bounds = [batch * c // self.chunks for c in range(self.chunks + 1)]
+            self.split = [batch * j // world for j in range(world + 1)]
+            self.mine = self.split[rank + 1] - self.split[rank]
+            self._plans = {}
+            return
         ld = plan.slab_ld
         self.slab = (torch.zeros((batch, ld), dtype=dtype, device=device)
                      if exchange != "p2p" else None)
@@ -325,7 +307,10 @@ class ShardedMapLookup:
         return peers, offs
 
     def close(self):
-        """Unmap the peers' destinations (p2p exchange)."""
+        """Release the native step (stream, events, RCCL communicator) or unmap the peers'
+        destinations (p2p exchange)."""
+        if self._native is not None:
+            self._native.close()
         if getattr(self, "_peers", None):
             L = _lib.load()
             for p, o in zip(self._peers, self._peer_offs):
@@ -398,6 +383,12 @@ class ShardedMapLookup:
         return self.out
 
     # --- the exchange -------------------------------------------------------------------
+    def _nccl_group(self) -> bool:
+        import torch.distributed as dist
+
+        return dist.is_available() and dist.is_initialized() and \
+            dist.get_backend(self.group) == "nccl"
+
     def _gloo(self) -> bool:
         import torch.distributed as dist
 
@@ -438,6 +429,8 @@ class ShardedMapLookup:
     def __call__(self, piece_tables, piece_idx, dst: torch.Tensor) -> torch.Tensor:
         """Run the sharded step; ``dst`` is ``(B, k + sum D)`` (allgather) or this
         rank's ``(B_r, k + sum D)`` batch slice (alltoall); p2p returns ``self.out``."""
+        if self._native is not None:
+            return self._native(piece_tables, piece_idx, dst)
         if self.exchange_kind == "p2p":
             return self._call_p2p(piece_tables, piece_idx, dst)
         if self.exchange_kind == "alltoall":
@@ -497,7 +490,13 @@ class ShardedMapLookup:
         from .update import SparseEmbeddingUpdate
 
         ps = self.plan.pieces[self.rank]
-        if self.exchange_kind in ("allgather", "p2p"):
+        if self._native is not None and self.exchange_kind == "alltoall":
+            recv = self._native.piece_grads(delta)
+            views, s = [], 0
+            for p in ps:
+                views.append(recv[:, s:s + p.dim])
+                s += p.dim
+        elif self.exchange_kind in ("allgather", "p2p"):
             views = [delta[:, p.col:p.col + p.dim] for p in ps]
         else:
             import torch.distributed as dist
@@ -524,6 +523,107 @@ class ShardedMapLookup:
                 s += p.dim
         return [SparseEmbeddingUpdate(t.lookup_type, v, i)
                 for t, v, i in zip(piece_tables, views, piece_idx)]
+
+
+class NativeShardedStep:
+    """The sharded step through the C ABI (et_sharded_create / et_sharded_maplookup /
+    et_sharded_piece_grads, csrc/et_shard.cpp): plan, pipelined lookup -> RCCL exchange ->
+    assembly, all native; Python only hands over pointers.  The RCCL communicator is made
+    with et_comm_unique_id / et_comm_init, the id broadcast over ``group``."""
+
+    def __init__(self, plan: ShardPlan, rank: int, world: int, batch: int, dtype, device,
+                 group=None, exchange: str = "allgather", chunks: int = 1, rccl: bool = True):
+        self.plan, self.rank, self.world, self.batch = plan, rank, world, batch
+        self.device, self.exchange = device, exchange
+        self.L = L = _lib.load()
+        self._et_dtype = _lib.TORCH_TO_ET[dtype]
+        self.comm = ctypes.c_void_p(None)
+        with torch.cuda.device(device):
+            if rccl:
+                self.comm = make_comm(group, rank, world)
+            flat = [p for r in range(world) for p in plan.pieces[r]]
+            arr = (_lib.ShardPiece * max(1, len(flat)))()
+            for i, (r, p) in enumerate((r, p) for r in range(world) for p in plan.pieces[r]):
+                arr[i] = _lib.ShardPiece(r, p.table, p.f0, p.dim, p.col)
+            h = ctypes.c_void_p()
+            kind = (_lib.ET_EXCHANGE_ALLTOALL if exchange == "alltoall"
+                    else _lib.ET_EXCHANGE_ALLGATHER)
+            _lib.check(L.et_sharded_create(ctypes.byref(h), self.comm, world, rank,
+                                           self._et_dtype, ctypes.addressof(arr), len(flat),
+                                           plan.prependrows, plan.ld, batch, chunks, kind))
+            self.h = h
+            ld, ws, lo, hi = (ctypes.c_int64() for _ in range(4))
+            _lib.check(L.et_sharded_info(h, ctypes.byref(ld), ctypes.byref(ws), ctypes.byref(lo),
+                                         ctypes.byref(hi)))
+            self.slab_ld, self.lo, self.hi = ld.value, lo.value, hi.value
+            self.workspace = torch.empty(ws.value, dtype=torch.uint8, device=device)
+        self._descs = {}
+
+    def _local_descs(self, piece_tables, piece_idx):
+        key = (tuple((id(t), t.device_table()) for t in piece_tables),
+               tuple((i.data_ptr(), tuple(i.shape), tuple(i.stride())) for i in piece_idx))
+        hit = self._descs.get(key)
+        if hit is not None:
+            return hit
+        from .lookup import _check_idx, _check_table, _ld
+
+        n = len(piece_tables)
+        descs = (_lib.LookupDesc * max(1, n))()
+        for j, (A, i) in enumerate(zip(piece_tables, piece_idx)):
+            _check_table(A)
+            _check_idx(i)
+            D, R = A.size()
+            table, cpp = A.device_table()
+            pool = 1 if i.dim() == 1 else int(i.shape[1])
+            descs[j] = _lib.LookupDesc(table, A.ld, R, D, pool, i.data_ptr(),
+                                       1 if i.dim() == 1 else _ld(i), 0, cpp)
+        if len(self._descs) >= 64:
+            self._descs.clear()
+        self._descs[key] = (descs, n, (piece_tables, piece_idx))
+        return self._descs[key]
+
+    def __call__(self, piece_tables, piece_idx, dst):
+        descs, n, _ = self._local_descs(piece_tables, piece_idx)
+        _lib.check(self.L.et_sharded_maplookup(
+            self.h, ctypes.addressof(descs), n, dst.data_ptr(), _ld(dst),
+            self.workspace.data_ptr(), self.workspace.numel(), _lib.ET_FLAG_NONTEMPORAL,
+            _lib.stream_handle(dst.device)))
+        return dst
+
+    def piece_grads(self, delta):
+        recv = torch.empty((self.batch, self.slab_ld), dtype=delta.dtype, device=delta.device)
+        _lib.check(self.L.et_sharded_piece_grads(
+            self.h, delta.data_ptr(), _ld(delta), recv.data_ptr(), self.workspace.data_ptr(),
+            self.workspace.numel(), _lib.stream_handle(delta.device)))
+        return recv
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.check(self.L.et_sharded_destroy(self.h))
+            self.h = None
+        if self.comm:
+            _lib.check(self.L.et_comm_destroy(self.comm))
+            self.comm = ctypes.c_void_p(None)
+
+
+def make_comm(group, rank: int, world: int) -> ctypes.c_void_p:
+    """An RCCL communicator over the ranks of ``group`` through the C ABI: rank 0's
+    et_comm_unique_id, broadcast by torch.distributed, then et_comm_init on every rank
+    (on the current device).  World 1 needs no broadcast."""
+    L = _lib.load()
+    idbuf = (ctypes.c_char * _lib.ET_COMM_ID_BYTES)()
+    if rank == 0:
+        _lib.check(L.et_comm_unique_id(ctypes.addressof(idbuf)))
+    if world > 1:
+        import torch.distributed as dist
+
+        obj = [bytes(idbuf) if rank == 0 else None]
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast_object_list(obj, src=src, group=group)
+        idbuf = (ctypes.c_char * _lib.ET_COMM_ID_BYTES).from_buffer_copy(obj[0])
+    comm = ctypes.c_void_p()
+    _lib.check(L.et_comm_init(ctypes.byref(comm), world, ctypes.addressof(idbuf), rank))
+    return comm
 
 
 class ShardedPreallocation(ShardedMapLookup):

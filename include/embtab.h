@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 5
+#define ET_ABI_VERSION 6
 
 /* Status codes. */
 #define ET_OK 0
@@ -270,6 +270,87 @@ int et_push_cols(int dtype, const void* src, int64_t ld, int64_t batch, int64_t 
 int et_ipc_handle(const void* ptr, void* handle, int64_t* offset);
 int et_ipc_open(const void* handle, int64_t offset, void** ptr);
 int et_ipc_close(void* ptr, int64_t offset);
+
+/* ---------------------------------------------------------------------------------
+ * Sharded PreallocationStrategy maplookup over the GPUs of a node (BASELINE config 5;
+ * SURVEY.md §8e).  No counterpart exists in the single-process reference: these replace
+ * the in-place concat of maplookup!(::PreallocationStrategy, dst, tables, I)
+ * (src/lookup.jl:316-371, the row-block views at :334-340) when the tables are spread
+ * over ranks — one process per GPU, RCCL over xGMI for the one exchange step.
+ * ------------------------------------------------------------------------------- */
+
+/* One piece of a shard plan: features [f0, f0+dim) of table `table` (0-based), owned by
+ * `rank`; its rows of the destination start at `col` (prependrows included). */
+typedef struct et_shard_piece {
+    int32_t rank;
+    int32_t table;
+    int32_t f0;
+    int32_t dim;
+    int64_t col;
+} et_shard_piece;
+
+#define ET_PLAN_TABLEWISE 0   /* whole tables, contiguous groups balanced by count (26 tables
+                                 on 8 GPUs: 4,4,3,3,3,3,3,3); with `sizes`, dealt in
+                                 descending size round-robin so the largest land on
+                                 distinct ranks */
+#define ET_PLAN_FEATUREWISE 1 /* the concatenated feature axis cut into equal contiguous
+                                 ranges at `granule`-feature boundaries inside tables, each
+                                 range cut into vector-kernel widths (96 -> 64 + 32) */
+
+/* The shard plan: every rank's pieces, rank by rank, each rank's in slab order.  With
+ * out == NULL only *npieces is set (the count to allocate).  Host-only; no device. */
+int et_shard_plan(int32_t mode, int32_t ntables, const int32_t* dims, const int64_t* sizes,
+                  int32_t world, int64_t prependrows, int32_t granule, int32_t elsize,
+                  et_shard_piece* out, int32_t cap, int32_t* npieces);
+
+/* RCCL communicator of the ranks (one process per GPU, the current HIP device):
+ * rank 0 creates a 128-byte id, the host broadcasts it by any means (MPI, a TCP store,
+ * torch.distributed), every rank calls et_comm_init with it.  The comm is a
+ * ncclComm_t; any ncclComm_t the host already owns may be passed instead. */
+#define ET_COMM_ID_BYTES 128
+int et_comm_unique_id(void* id);
+int et_comm_init(void** comm, int32_t nranks, const void* id, int32_t rank);
+int et_comm_destroy(void* comm);
+
+/* The exchange step on its own: ncclAllGather of every rank's (slab_ld x batch) slab into
+ * `gathered` (nranks slabs, rank after rank), then et_concat_slabs(gathered, rows,
+ * dst_row_off) into dst.  One contiguous run of destination rows per rank.  comm == NULL
+ * (allowed for nranks == 1 only) copies the slab instead of calling RCCL. */
+int et_allgather_concat(void* comm, int dtype, const void* slab, int64_t slab_ld, int64_t batch,
+                        void* gathered, int32_t nranks, const int32_t* rows,
+                        const int64_t* dst_row_off, void* dst, int64_t ld_dst, void* stream);
+
+#define ET_EXCHANGE_ALLGATHER 0 /* every rank ends with the whole (ld_dst x batch) dst */
+#define ET_EXCHANGE_ALLTOALL 1  /* DLRM layout: rank r ends with bags [r*B/N, (r+1)*B/N) of
+                                   every feature (N times less on the links) */
+
+/* A sharded step: the plan (all ranks' pieces, as from et_shard_plan), this rank, the
+ * destination geometry, `chunks` batch chunks pipelined through lookup / exchange /
+ * assembly (all-gather only).  comm may be NULL only for world == 1 (the exchange is then
+ * a device copy).  Creates one side stream and a few events on the current device;
+ * everything else is caller-owned. */
+int et_sharded_create(void** handle, void* comm, int32_t world, int32_t rank, int dtype,
+                      const et_shard_piece* pieces, int32_t npieces, int64_t prependrows,
+                      int64_t ld_dst, int64_t batch, int32_t chunks, int32_t exchange);
+/* Slab leading dimension, workspace bytes, and the bags [lo, hi) of dst this rank ends
+ * with (0..batch for the all-gather). */
+int et_sharded_info(void* handle, int64_t* slab_ld, int64_t* ws_bytes, int64_t* batch_lo,
+                    int64_t* batch_hi);
+/* One step: `local` holds this rank's pieces in plan order (table = the piece's columns,
+ * e.g. a column-slice pointer with the parent's ld_table; dim = the piece's dim; idx for
+ * the whole batch; dst_row_off ignored).  Stream-ordered on `stream`; dst is
+ * (ld_dst x batch), or (ld_dst x (hi - lo)) for the all-to-all. */
+int et_sharded_maplookup(void* handle, const et_lookup_desc* local, int32_t nlocal, void* dst,
+                         int64_t ld_dst, void* workspace, int64_t ws_bytes, uint32_t flags,
+                         void* stream);
+/* Backward of the all-to-all layout (rrule of the sharded maplookup, src/lookup.jl:374-389):
+ * from this rank's (ld_delta x (hi - lo)) gradient slice, every rank's feature rows are cut
+ * out (et_split_slabs) and exchanged, giving `recv` = (slab_ld x batch): this rank's
+ * pieces' gradient rows for every bag, pieces in plan order.  (Under the all-gather layout
+ * the gradient is replicated and a piece's gradient is a row block of it.) */
+int et_sharded_piece_grads(void* handle, const void* delta, int64_t ld_delta, void* recv,
+                           void* workspace, int64_t ws_bytes, void* stream);
+int et_sharded_destroy(void* handle);
 
 /* Deterministic synthetic data (the same counter-based hash as oracle/):
  * element i of dst = lo + (hi-lo) * u(seed, offset + i), u in [0,1) with 24 bits. */

@@ -37,7 +37,7 @@ def test_abi_version_and_last_error():
     from embtab import _lib
 
     L = _lib.load()
-    assert L.et_abi_version() == _lib.ET_ABI_VERSION == 5
+    assert L.et_abi_version() == _lib.ET_ABI_VERSION == 6
     assert isinstance(L.et_last_error(), bytes)
 
 
@@ -55,18 +55,22 @@ int main(void) {
          sizeof(et_update_desc));
   printf("%zu %zu %zu\n", offsetof(et_update_desc, delta), offsetof(et_update_desc, idx),
          offsetof(et_update_desc, batch));
+  printf("%zu %zu %zu\n", sizeof(et_shard_piece), offsetof(et_shard_piece, dim),
+         offsetof(et_shard_piece, col));
   return 0;
 }
 ''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(prog), "-o", str(exe)],
                    check=True)
-    l1, l2 = subprocess.run([str(exe)], capture_output=True, text=True,
-                            check=True).stdout.split("\n")[:2]
+    l1, l2, l3 = subprocess.run([str(exe)], capture_output=True, text=True,
+                                check=True).stdout.split("\n")[:3]
     L, U = _lib.LookupDesc, _lib.UpdateDesc
     assert list(map(int, l1.split())) == [ctypes.sizeof(L), L.dim.offset, L.idx.offset,
                                           L.dst_row_off.offset, ctypes.sizeof(U)]
     assert list(map(int, l2.split())) == [U.delta.offset, U.idx.offset, U.batch.offset]
+    S = _lib.ShardPiece
+    assert list(map(int, l3.split())) == [ctypes.sizeof(S), S.dim.offset, S.col.offset]
 
 
 def test_argument_errors_need_no_gpu():
@@ -125,3 +129,33 @@ def test_phase_flags_need_no_gpu():
         sizes.append(nb.value)
     # the dim-128 pool-20 table carries 120 slots x 4 windows x 512 B of window partials
     assert sizes[0] > 120 * 4 * 512 + 20 * 4096 * 16
+
+
+def test_shard_plan_is_host_only():
+    """et_shard_plan: SURVEY.md §8e's 26-table split, argument errors, count query."""
+    from embtab import _lib
+    from embtab.sharding import native_plan
+
+    L = _lib.load()
+    p = native_plan(_lib.ET_PLAN_TABLEWISE, [128] * 26, 8)
+    assert [len(x) for x in p] == [4, 4, 3, 3, 3, 3, 3, 3]
+    assert [q.col for x in p for q in x] == [128 * t for t in range(26)]
+    f = native_plan(_lib.ET_PLAN_FEATUREWISE, [128] * 26, 8, prependrows=16)
+    assert [sum(q.dim for q in x) for x in f] == [416] * 8
+    assert all(q.dim in (32, 64, 128) and q.col >= 16 for x in f for q in x)
+    dims = (ctypes.c_int32 * 2)(5, 7)
+    n = ctypes.c_int32(0)
+    assert L.et_shard_plan(0, 2, ctypes.addressof(dims), None, 0, 0, 32, 4, None, 0,
+                           ctypes.byref(n)) == -1
+    assert L.et_shard_plan(7, 2, ctypes.addressof(dims), None, 2, 0, 32, 4, None, 0,
+                           ctypes.byref(n)) == -1
+    assert L.et_shard_plan(1, 2, ctypes.addressof(dims), None, 2, 0, 32, 4, None, 0,
+                           ctypes.byref(n)) == 0 and n.value == 2
+    one = (_lib.ShardPiece * 1)()
+    assert L.et_shard_plan(1, 2, ctypes.addressof(dims), None, 2, 0, 32, 4,
+                           ctypes.addressof(one), 1, ctypes.byref(n)) == -1
+    # a sharded step without a communicator is world 1 only
+    h = ctypes.c_void_p()
+    assert L.et_sharded_create(ctypes.byref(h), None, 2, 0, _lib.ET_F32, None, 0, 0, 16, 8, 1,
+                               0) == -1
+    assert b"communicator" in L.et_last_error()

@@ -358,6 +358,76 @@ def test_sharded_prealloc_single_rank(oracle):
             assert bits_equal(host(dst)[:, 4:], ref[:, 4:])
 
 
+@pytest.mark.parametrize("exchange,chunks", [("allgather", 1), ("allgather", 4),
+                                             ("alltoall", 1)])
+def test_native_sharded_step_rccl_world1(oracle, exchange, chunks):
+    """The C-ABI sharded step (et_sharded_create / et_sharded_maplookup, csrc/et_shard.cpp)
+    with a real RCCL communicator of one rank (et_comm_unique_id / et_comm_init), so the
+    ncclAllGather / ncclSend-ncclRecv calls execute: equals the unsharded Preallocation
+    (src/lookup.jl:316-371) bit for bit; the all-to-all backward returns the gradient rows
+    of the rank's pieces."""
+    from embtab.sharding import ShardedMapLookup, ShardPlan
+
+    rng = np.random.default_rng(81)
+    dims = [128, 64, 128, 96]
+    rows = [300, 5000, 20, 800]
+    B, k = 300, 4
+    hs = [rng.random((r, d), dtype=np.float32) for r, d in zip(rows, dims)]
+    hidx = [rng.integers(1, r + 1, (B, 20)) for r in rows]
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=k)
+    for plan in (ShardPlan.tablewise(dims, 1, k), ShardPlan.featurewise(dims, 1, k)):
+        sm = ShardedMapLookup(plan, 0, 1, B, torch.float32, DEV, exchange=exchange,
+                              chunks=chunks, rccl=True)
+        assert sm._native is not None and sm._native.comm
+        try:
+            dst = torch.zeros((B, plan.ld), dtype=torch.float32, device=DEV)
+            from embtab.sharding import piece_table
+            full = [table(h) for h in hs]
+            ps = plan.pieces[0]
+            sm([piece_table(full[p.table], p) for p in ps], [dev(hidx[p.table]) for p in ps], dst)
+            torch.cuda.synchronize()
+            assert bits_equal(host(dst)[:, k:], ref[:, k:])
+            if exchange == "alltoall":
+                delta = dev(rng.standard_normal((B, plan.ld)).astype(np.float32))
+                grads = sm.piece_grads([piece_table(full[p.table], p) for p in ps],
+                                       [dev(hidx[p.table]) for p in ps], delta)
+                for p, g in zip(ps, grads):
+                    assert torch.equal(g.delta, delta[:, p.col:p.col + p.dim])
+        finally:
+            sm.close()
+
+
+def test_allgather_concat_rccl_world1():
+    """et_allgather_concat on a one-rank RCCL communicator: ncclAllGather + assembly."""
+    import ctypes
+
+    from embtab import _lib
+
+    L = _lib.load()
+    idb = (ctypes.c_char * _lib.ET_COMM_ID_BYTES)()
+    _lib.check(L.et_comm_unique_id(ctypes.addressof(idb)))
+    comm = ctypes.c_void_p()
+    _lib.check(L.et_comm_init(ctypes.byref(comm), 1, ctypes.addressof(idb), 0))
+    try:
+        rng = np.random.default_rng(3)
+        B, slab_ld, ld = 1000, 40, 50
+        slab = dev(rng.standard_normal((B, slab_ld)).astype(np.float32))
+        gathered = torch.empty_like(slab)
+        dst = torch.zeros((B, ld), dtype=torch.float32, device=DEV)
+        rows = np.array([37], np.int32)
+        offs = np.array([9], np.int64)
+        _lib.check(L.et_allgather_concat(comm, _lib.ET_F32, slab.data_ptr(), slab_ld, B,
+                                         gathered.data_ptr(), 1, rows.ctypes.data,
+                                         offs.ctypes.data, dst.data_ptr(), ld,
+                                         _lib.stream_handle()))
+        torch.cuda.synchronize()
+        assert torch.equal(gathered, slab)
+        assert torch.equal(dst[:, 9:46], slab[:, :37])
+        assert not dst[:, :9].any() and not dst[:, 46:].any()
+    finally:
+        _lib.check(L.et_comm_destroy(comm))
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_pieces_simulated_ranks(oracle, world):
     """Feature-sharded plans on the real kernels: every simulated rank looks up its
