@@ -545,3 +545,4 @@ def test_update_hot_column_pass_multi_table(oracle):
         exact_upd, scale = _fp64_update_and_scale(bases[k], delta[:, 8 + k * D:8 + (k + 1) * D],
                                                   hidx[k])
         assert np.all(np.abs(out[k].astype(np.float64) - exact_upd) <= 1e-6 * scale), k
+    assert et.check_errors() == 6  # the 3 skipped entries, counted by both runs
