@@ -847,11 +847,21 @@ __global__ __launch_bounds__(256) void k_sgd_combine_generic(
         const int t = table_of_key(pack, ntables, key);
         const et_update_desc& d = pack.d[t];
         if ((pack.vec_mask >> t) & 1u) continue;
+        // the vector combine's fixed partition (k_sgd_combine: 8 contiguous ranges of
+        // partials, each summed from 0, the range sums added in order), so a table taking
+        // the generic path combines exactly like a vector-width feature slice of it
+        const uint32_t np = p1 - p0;
         for (int f = lane; f < d.dim; f += 64) {
-            C acc = C(0);
-            for (uint32_t q = p0; q < p1; ++q) acc = acc + partials[(uint64_t)q * pdim + f];
+            C tot = C(0);
+            for (int R = 0; R < 8; ++R) {
+                const uint32_t a = p0 + (uint32_t)((uint64_t)np * R / 8);
+                const uint32_t b = p0 + (uint32_t)((uint64_t)np * (R + 1) / 8);
+                C acc = C(0);
+                for (uint32_t q = a; q < b; ++q) acc = acc + partials[(uint64_t)q * pdim + f];
+                tot = tot + acc;
+            }
             T* w = col_ptr<T>(d.table, d.ld_table, d.cols_per_page, key - pack.row_off[t]) + f;
-            store_scalar<NT>(w, sgd_apply_t<T, C, MODE>(*w, acc, eta_c, eta64));
+            store_scalar<NT>(w, sgd_apply_t<T, C, MODE>(*w, tot, eta_c, eta64));
         }
     }
 }
@@ -1258,17 +1268,21 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         // paged tables qualify too: their pages are 16-byte aligned by contract
         // vector kernels at the power-of-two capacity of the dim (masked below it)
         const int cap = et::vec_dim_ok(d.dim) ? d.dim : et::masked_capacity(d.dim);
-        const bool vec_ok = dtype == ET_F32 && (d.cols_per_page > 0 || et::aligned16(d.table)) &&
-                            et::aligned16(d.delta) && (d.ld_table % 4 == 0) &&
-                            (d.ld_delta % 4 == 0) && d.dim % 4 == 0 && d.dim <= 2048 &&
-                            vg.add(cap, t);
-        if (vec_ok) {
+        const bool table_ok = dtype == ET_F32 && (d.cols_per_page > 0 || et::aligned16(d.table)) &&
+                              (d.ld_table % 4 == 0) && d.dim % 4 == 0 && d.dim <= 2048;
+        const bool delta_ok = et::aligned16(d.delta) && (d.ld_delta % 4 == 0);
+        // hot-column pass (Float32 vector tables of dim 128, non-exact mode): chosen from
+        // the table alone, so the index phase (which never sees the gradient, delta may be
+        // NULL) and the update phase agree; the update phase then needs vector gradients
+        const bool hot = table_ok && !exact && (flags & ET_FLAG_SGD_HOT_PASS) && et::hot_shape(d);
+        if (hot) {
+            if (apply_only && !delta_ok)
+                return et::fail(ET_ERR_ARG, "table %d: the hot-column pass chosen by the index "
+                                            "phase needs a 16-byte aligned gradient (ld %% 4 == 0)", t);
+            if (index_only || delta_ok) hot_mask |= 1u << t;
+        }
+        if (table_ok && (delta_ok || index_only) && vg.add(cap, t)) {
             pack.vec_mask |= 1u << t;
-            // hot-column pass: Float32 vector tables of dim 128, non-exact mode, float2
-            // gradient loads (identical in both phases for the same descriptors)
-            if (!exact && (flags & ET_FLAG_SGD_HOT_PASS) && et::hot_shape(d) &&
-                (reinterpret_cast<uintptr_t>(d.delta) & 7u) == 0 && d.ld_delta % 2 == 0)
-                hot_mask |= 1u << t;
         } else {
             any_generic = true;
         }

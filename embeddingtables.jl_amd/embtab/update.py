@@ -4,7 +4,7 @@ Mirrors (darchr/EmbeddingTables.jl):
   SparseEmbeddingUpdate / uncompress         src/sparseupdate.jl:6-32
   rrule(lookup)                              src/sparseupdate.jl:35-40
   rrule(maplookup, strategy) (+ Slicer)      src/lookup.jl:247-258, :374-389, src/utils.jl:50-63
-  update!(table, grad, indexer, alpha, Val)  src/sparseupdate.jl:436-544 (specialized/generic)
+  update!(table, grad, indexer, alpha, Val)  src/sparseupdate.jl:46-154 (generic/specialized)
   update!(::Descent, table, grad, ...)       src/sparseupdate.jl:160-178
   Flux.Optimise.update!(opt, x, xbar, ...)   src/sparseupdate.jl:180-189
   multi-table update!(opt, tables, grads, indexers; num_splits, ...)  :199-238
@@ -137,9 +137,50 @@ class Indexer(AbstractIndexer):
     flavour = "sparse"
 
     def __init__(self):
-        self.cumulative = None
-        self.map = None
-        self.nunique = 0
+        self._cumulative = None
+        self._map = None
+        self._nunique = 0
+        self._pending = None  # (indices, maxindex) of a multi-table update!, built on use
+
+    def _defer(self, indices, maxindex: int):
+        """The multi-table ``update!`` fills every ``indexers[i]`` in its index phase
+        (src/sparseupdate.jl:210-213).  The device update indexes all tables in its own
+        fused pipeline, so the reference-layout Indexer is built from the same index
+        array on first use (et_index_build) instead of on every step."""
+        self._pending = (indices, int(maxindex))
+
+    def _materialise(self):
+        if self._pending is not None:
+            indices, maxindex = self._pending
+            self._pending = None
+            index_(self, indices, maxindex)
+
+    @property
+    def cumulative(self):
+        self._materialise()
+        return self._cumulative
+
+    @cumulative.setter
+    def cumulative(self, v):
+        self._cumulative = v
+
+    @property
+    def map(self):
+        self._materialise()
+        return self._map
+
+    @map.setter
+    def map(self, v):
+        self._map = v
+
+    @property
+    def nunique(self):
+        self._materialise()
+        return self._nunique
+
+    @nunique.setter
+    def nunique(self, v):
+        self._nunique = v
 
     @property
     def histogram(self):
@@ -190,6 +231,7 @@ def index_(indexer: Indexer, A: torch.Tensor, maxindex: int) -> Indexer:
                                 nu.data_ptr(), ws.data_ptr(), ws.numel(),
                                 _lib.stream_handle(dev)))
     U = int(nu.item())
+    indexer._pending = None
     indexer.nunique = U
     indexer.cumulative = cum[:, :U + 1].t()
     indexer.map = mp[:n]
@@ -264,7 +306,7 @@ def update_(*args, nontemporal: bool | None = None, exact: bool = False,
     * ``update_(opt::Descent, tables, grads, indexers, [nontemporal]; num_splits, nthreads,
       scratchspaces, telemetry_cb)`` — all tables in one pipeline (:199-238);
     * ``update_(table, grad, indexer_or_view, alpha, [nontemporal])`` — update from a
-      prebuilt Indexer / IndexerView range (:436-544).
+      prebuilt Indexer / IndexerView range (:46-154).
 
     ``exact=True`` sums every column's gradient serially (bit-identical to the
     reference even for hot columns); the default splits occurrence lists longer than
@@ -282,6 +324,8 @@ def update_(*args, nontemporal: bool | None = None, exact: bool = False,
             return None
         tables, grads = list(args[1]), list(args[2])
         nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
+        if len(args) > 3 and args[3] is not None:
+            kw["indexers"] = args[3]
         _update_multi(opt, tables, grads, nt, exact, f16_fp32_acc, hot_pass=hot_pass, **kw)
         return None
     table, grad, indexer, alpha = args[:4]
@@ -305,10 +349,21 @@ def _update_single(opt: Descent, table, grad: SparseEmbeddingUpdate, nontemporal
 def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
                   f16_fp32_acc: bool = False, num_splits=4, nthreads=None, scratchspaces=None,
                   telemetry_cb=None, indexers=None, hot_pass: bool = False):
+    """src/sparseupdate.jl:199-238: index every table, ``telemetry_cb()``, then update
+    every table.  Both phases are one device pipeline per (path, eltype) group of at
+    most ET_MAX_TABLES_PER_LAUNCH tables (ET_FLAG_SGD_INDEX_ONLY, then
+    ET_FLAG_SGD_APPLY_ONLY from the same workspace); ``telemetry_cb`` runs on the host
+    once the index phase is enqueued (stream order puts it between the phases, as the
+    reference's call between its two threaded loops).  ``indexers[i]`` receives table
+    i's Indexer (built from ``grads[i].indices`` on first use — see Indexer._defer).
+    ``num_splits`` / ``nthreads`` / ``scratchspaces`` only shape the reference's CPU work
+    queue and have no device counterpart."""
     if len(tables) != len(grads):
         raise ArgumentError("tables and grads differ in length")
-    if telemetry_cb is not None:
-        telemetry_cb()
+    if indexers is not None:
+        indexers = list(indexers)
+        if len(indexers) != len(grads):
+            raise ArgumentError("indexers and grads differ in length")
     # Group tables by the reference's per-table path: Static <= 512 B -> specialized
     # (Float32 eta, fused); otherwise generic with the unconverted Float64 eta
     # (src/sparseupdate.jl:232).
@@ -317,13 +372,35 @@ def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
         if g.indices.numel() == 0:
             continue
         groups.setdefault((fused_update_path(A), A.dtype), []).append(_update_desc(A, g))
-    if not groups:
-        return
-    dev = tables[0].device
-    for (fused, dtype), descs in groups.items():
-        flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc, hot_pass)
-        for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
-            _sparse_sgd(descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH], opt.eta, flags, dev, dtype)
+    calls = []
+    if groups:
+        dev = tables[0].device
+        L = _lib.load()
+        stream = _lib.stream_handle(dev)
+        for (fused, dtype), descs in groups.items():
+            flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc, hot_pass)
+            for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
+                part = descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH]
+                arr = (_lib.UpdateDesc * len(part))(*part)
+                nb = ctypes.c_int64(0)
+                _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), len(part),
+                                                   ctypes.byref(nb)))
+                ws = _workspace(nb.value, dev, f"sgd{len(calls)}")
+                calls.append((_lib.TORCH_TO_ET[dtype], arr, len(part), flags, ws))
+        for et_t, arr, n, flags, ws in calls:  # phase 1: index all tables
+            _lib.check(L.et_sparse_sgd(et_t, ctypes.addressof(arr), n, float(opt.eta),
+                                       flags | _lib.ET_FLAG_SGD_INDEX_ONLY, ws.data_ptr(),
+                                       ws.numel(), stream))
+    if indexers is not None:
+        for ix, A, g in zip(indexers, tables, grads):
+            if isinstance(ix, Indexer):
+                ix._defer(g.indices, A.size()[1])
+    if telemetry_cb is not None:
+        telemetry_cb()
+    for et_t, arr, n, flags, ws in calls:  # phase 2: update all tables
+        _lib.check(L.et_sparse_sgd(et_t, ctypes.addressof(arr), n, float(opt.eta),
+                                   flags | _lib.ET_FLAG_SGD_APPLY_ONLY, ws.data_ptr(),
+                                   ws.numel(), stream))
 
 
 def _update_from_indexer(table, grad: SparseEmbeddingUpdate, indexer: AbstractIndexer,

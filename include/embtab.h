@@ -204,7 +204,7 @@ int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, doubl
 /* Update from a prebuilt Indexer (et_index_build layout) over its cumulative entries
  * [ubegin, uend) — the reference's lower-level
  * update!(table, ::SparseEmbeddingUpdate, indexer::AbstractIndexer, alpha, Val(NT)),
- * src/sparseupdate.jl:436-544, where an IndexerView (src/utils.jl:320-338) selects a
+ * src/sparseupdate.jl:46-154, where an IndexerView (src/utils.jl:320-338) selects a
  * range of distinct columns.  Every column's gradient is summed serially in `map`
  * order (exact).  `cumulative_*` and `map` are device arrays as written by
  * et_index_build; `eta` is the value the reference passes as `alpha`;

@@ -494,10 +494,13 @@ def test_sharded_training_step_simulated_ranks(oracle, exact):
     from embtab.sharding import ShardedMapLookup, ShardPlan, piece_table
 
     rng = np.random.default_rng(44)
-    dims, rows, B, P = [128, 128, 64, 128], [3000, 40, 700, 9000], 512, 20
+    # dim 50 (not a multiple of 4) takes the generic kernels as a whole table, while its
+    # 32-feature slice takes the vector ones: both combine > 8 partials identically
+    dims, rows, B, P = [128, 128, 64, 128, 50], [3000, 40, 700, 9000, 900], 512, 20
     hs = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
     hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
     hidx[1][:, :5] = 2  # a hot column (2560 occurrences)
+    hidx[4][:, :5] = 3  # and one in the generic-path table
     didx = [dev(i) for i in hidx]
     delta = dev(rng.standard_normal((B, sum(dims))).astype(np.float32))
     ref = [et.SimpleEmbedding(dev(h), et.Static(h.shape[1])) for h in hs]

@@ -1,6 +1,6 @@
 """Paged tables (the reference's SplitEmbedding, src/split.jl) on the HIP path.
 
-Mirrors test/lookup.jl:110-140 ("Testing Standard Split" / "Testing Reducing Split":
+Mirrors test/lookup.jl:110-139 ("Testing Standard Split" / "Testing Reducing Split":
 dims 32..1504, 1000 columns, chunk sizes 10..50, permutations and repeats, 12 lookups
 per output): every result is bit-identical to the oracle run on the dense table.
 The update cases check that a paged table receives exactly the dense update."""

@@ -80,7 +80,7 @@ def test_update_exact_vs_oracle(oracle, dim, static, reducing):
     ref = base.copy()
     oracle.sgd(ref, delta, I, 10.0, fused=fused_update_path(A))
     assert bits_equal(host(A.data), ref)
-    # uncompress vs a dense scatter (test/update.jl:294-295)
+    # uncompress vs a dense scatter (test/update.jl:44-45)
     dense = host(et.uncompress(g, ncols))
     acc = np.zeros((ncols, dim), np.float64)
     Ib = I.reshape(ncols, -1)
@@ -91,9 +91,13 @@ def test_update_exact_vs_oracle(oracle, dim, static, reducing):
 
 
 def test_update_hot_rows_chunked_vs_exact(oracle):
-    """Zipf-skewed indices: occurrence lists longer than the ET_SGD_CHUNK-entry chunk are summed
-    as ordered partial sums (deterministic) — within 1e-6 rel of the serial sum; the
-    exact mode is bit-identical."""
+    """Zipf-skewed indices.  Exact mode: bit-identical to the reference's serial sum
+    (north_star's 1e-6-relative bound, met with zero error).  Default mode: columns with
+    at most ET_SGD_CHUNK occurrences are bit-identical too; longer occurrence lists are
+    summed as ordered partial sums (deterministic), whose error is bounded by 1e-6 of the
+    summation-error scale |w| + eta * sum|delta| of the exact (fp64) update and is no
+    larger — absolute or relative to the exact update — than the serial fp32 sum's own
+    error: the chunked result is as close to the true update as the reference's."""
     rng = np.random.default_rng(12)
     ncols, dim, B, P = 5000, 128, 4096, 20
     base = rng.standard_normal((ncols, dim)).astype(np.float32)
@@ -130,6 +134,10 @@ def test_update_hot_rows_chunked_vs_exact(oracle):
     err_serial = np.abs(ref.astype(np.float64) - exact_upd)
     assert np.all(err_chunked <= 1e-6 * scale)
     assert err_chunked[hot].max() <= err_serial[hot].max()
+    big = hot[:, None] & (np.abs(exact_upd) > 1.0)
+    rel_chunked = (err_chunked / np.abs(exact_upd))[big]
+    rel_serial = (err_serial / np.abs(exact_upd))[big]
+    assert big.any() and rel_chunked.max() <= rel_serial.max()
     # deterministic: the chunked result repeats exactly
     A = et.SimpleEmbedding(dev(base), et.Static(dim))
     et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), dev(I)))
@@ -183,7 +191,7 @@ def test_multi_table_update_vs_oracle(oracle, fused_dims):
 
 
 def test_map_gradients_structure():
-    """test/map.jl:530-589: grads through maplookup and PreallocationStrategy (with and
+    """test/map.jl:109-177: grads through maplookup and PreallocationStrategy (with and
     without prepended rows) carry the forward indices and equal deltas."""
     rng = np.random.default_rng(0)
     dims = [(5, 5), (5, 10), (5, 15)]
@@ -546,3 +554,91 @@ def test_update_hot_column_pass_multi_table(oracle):
                                                   hidx[k])
         assert np.all(np.abs(out[k].astype(np.float64) - exact_upd) <= 1e-6 * scale), k
     assert et.check_errors() == 6  # the 3 skipped entries, counted by both runs
+
+
+def test_multi_table_update_phases_telemetry_and_indexers(oracle):
+    """src/sparseupdate.jl:208-214: the multi-table update! indexes every table, calls
+    telemetry_cb() between its index phase and its update phase, and leaves table i's
+    Indexer in indexers[i].  Here: when the callback runs no table has been updated yet
+    (the update phase is not enqueued), afterwards all are, and every indexers[i] equals
+    et_index_build's Indexer of grads[i].indices (the reference's cumulative / map)."""
+    rng = np.random.default_rng(208)
+    dims, rows, B, P = [128, 64, 32], [500, 40, 3000], 300, 7
+    hs = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
+    tabs = [et.SimpleEmbedding(dev(h), et.Static(h.shape[1])) for h in hs]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    delta = rng.standard_normal((B, sum(dims))).astype(np.float32)
+    dd = dev(delta)
+    offs = np.cumsum([0] + dims[:-1])
+    grads = [et.SparseEmbeddingUpdate(t.lookup_type, dd[:, o:o + d], dev(i))
+             for t, o, d, i in zip(tabs, offs, dims, hidx)]
+    seen = []
+
+    def telemetry():
+        torch.cuda.synchronize()  # everything enqueued so far (the index phase) is done
+        seen.append([bits_equal(host(t.data), h) for t, h in zip(tabs, hs)])
+
+    indexers = [et.Indexer(), et.DenseIndexer(), et.SparseIndexer()]
+    et.update_(et.Descent(0.1), tabs, grads, indexers, telemetry_cb=telemetry)
+    assert seen == [[True, True, True]]
+    for t in range(3):
+        ref = hs[t].copy()
+        oracle.sgd(ref, np.ascontiguousarray(delta[:, offs[t]:offs[t] + dims[t]]), hidx[t], 0.1,
+                   fused=True)
+        assert bits_equal(host(tabs[t].data), ref)
+        fresh = et.index_(et.Indexer(), grads[t].indices, rows[t])
+        assert torch.equal(indexers[t].cumulative, fresh.cumulative)
+        assert torch.equal(indexers[t].map, fresh.map)
+        assert indexers[t].nunique == fresh.nunique
+        cum, mp = oracle.index_build(hidx[t], rows[t])
+        assert np.array_equal(host(indexers[t].cumulative), cum)
+        assert np.array_equal(host(indexers[t].map), mp)
+
+
+def test_phased_hot_pass_null_delta_index_phase():
+    """ET_FLAG_SGD_INDEX_ONLY with delta = NULL and the hot-column pass on: the index
+    phase picks the hot columns from the tables alone, the update phase with an aligned
+    gradient then equals the one-call update bit for bit; an update phase whose gradient
+    cannot take the vector path the index phase planned for is refused (ET_ERR_ARG)
+    before any device work."""
+    import ctypes
+
+    from embtab import _lib
+
+    L = _lib.load()
+    rng = np.random.default_rng(31)
+    B, P, D, R = 3000, 13, 128, 400
+    base = rng.standard_normal((R, D)).astype(np.float32)
+    I = np.minimum(rng.zipf(1.1, (B, P)), R)
+    delta = rng.standard_normal((B, D + 1)).astype(np.float32)
+    dI, dd = dev(I), dev(delta)
+    flags = _lib.ET_FLAG_NONTEMPORAL | _lib.ET_FLAG_SGD_HOT_PASS
+
+    def desc(tab, dptr, ld):
+        return _lib.UpdateDesc(tab.data_ptr(), D, R, D, P, dptr, ld, dI.data_ptr(), P, B, 0)
+
+    one = dev(base)
+    arr = (_lib.UpdateDesc * 1)(desc(one, dd.data_ptr(), D + 1))
+    # reference run: the same table through the one-call update with an aligned copy of Δ
+    al = dev(np.ascontiguousarray(delta[:, :D]))
+    arr[0] = desc(one, al.data_ptr(), D)
+    nb = ctypes.c_int64()
+    _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), 1, ctypes.byref(nb)))
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=DEV)
+    st = _lib.stream_handle()
+    _lib.check(L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(arr), 1, 0.1, flags, ws.data_ptr(),
+                               ws.numel(), st))
+    two = dev(base)
+    arr[0] = desc(two, 0, D)  # phase 1 never reads the gradient
+    _lib.check(L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(arr), 1, 0.1,
+                               flags | _lib.ET_FLAG_SGD_INDEX_ONLY, ws.data_ptr(), ws.numel(), st))
+    arr[0] = desc(two, dd.data_ptr() + 4, D + 1)  # misaligned: no vector path
+    rc = L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(arr), 1, 0.1,
+                         flags | _lib.ET_FLAG_SGD_APPLY_ONLY, ws.data_ptr(), ws.numel(), st)
+    assert rc == -1 and b"hot-column" in L.et_last_error()
+    arr[0] = desc(two, al.data_ptr(), D)
+    _lib.check(L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(arr), 1, 0.1,
+                               flags | _lib.ET_FLAG_SGD_APPLY_ONLY, ws.data_ptr(), ws.numel(), st))
+    torch.cuda.synchronize()
+    assert torch.equal(one, two)
+    assert not torch.equal(one, dev(base))

@@ -99,7 +99,7 @@ def test_lookup_vs_naive(oracle, dim):
     assert np.array_equal(oracle.lookup(A, perm), oracle.naive_lookup(A, perm))
     rep = rng.integers(1, ncols + 1, ncols)
     assert np.array_equal(oracle.lookup(A, rep), oracle.naive_lookup(A, rep))
-    # reducing: 12 lookups per output (test/lookup.jl:153), no repeats then repeats
+    # reducing: 12 lookups per output (test/lookup.jl:42), no repeats then repeats
     I = np.stack([rng.permutation(np.arange(2, ncols + 1)) for _ in range(12)], 1)
     assert np.array_equal(oracle.lookup(A, I), oracle.naive_lookup(A, I))
     I = rng.integers(1, ncols + 1, (ncols, 12))
