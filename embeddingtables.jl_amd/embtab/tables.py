@@ -84,8 +84,24 @@ class AbstractEmbeddingTable:
     """A D x R table of feature-contiguous columns on one GPU.
 
     Subtypes provide ``size()``, ``columnpointer(col, ctx)`` and ``example()``
-    (README.md:288-307); the engine additionally needs ``ld`` (elements between
-    columns) so that a kernel can address every column from the first one.
+    (README.md:288-307) — nothing else is required: the columns may sit anywhere in
+    device memory (README.md:305-307: "this does not impose any requirement on the
+    layout or ordering of the columns themselves").  ``device_table()`` turns the
+    ``columnpointer`` contract into a kernel descriptor once per table:
+
+    * equally spaced columns -> a contiguous descriptor (first column, ``ld`` = the
+      spacing in elements);
+    * anything else -> a device array of R column pointers, described as a paged table
+      with one column per page (``cols_per_page = 1``), the generalisation of the
+      SplitEmbedding page table.  16-byte aligned pointers (and a 16-byte multiple row)
+      keep the vector kernels; otherwise ``ld`` is set to a non-16-byte spacing, which
+      selects the generic (element-aligned) kernels — ``ld`` is never used to address a
+      one-column page.
+
+    Subtypes with a uniform layout (SimpleEmbedding, SplitEmbedding) override
+    ``device_table``/``ld``; a subtype may also override ``columnpointers()`` to hand
+    over all R pointers at once.  The descriptor is cached: call ``invalidate()`` after
+    moving a table's columns.
     """
 
     lookup_type: AbstractLookupType = Dynamic
@@ -99,10 +115,54 @@ class AbstractEmbeddingTable:
     def example(self) -> torch.Tensor:
         raise NotImplementedError
 
+    def columnpointers(self):
+        """Device addresses of columns 1..R (``columnpointer`` of each, by default)."""
+        _, R = self.size()
+        return [self.columnpointer(i) for i in range(1, R + 1)]
+
+    def invalidate(self):
+        self.__dict__.pop("_desc_cache", None)
+
+    def _describe(self):
+        c = self.__dict__.get("_desc_cache")
+        if c is not None:
+            return c
+        import numpy as np
+
+        D, R = self.size()
+        es = self.example().element_size()
+        if R == 0:
+            raise ArgumentError("a table needs at least one column")
+        p = np.asarray(self.columnpointers(), dtype=np.int64)
+        if len(p) != R:
+            raise ArgumentError(f"columnpointers() gave {len(p)} pointers for {R} columns")
+        if R == 1:
+            c = (int(p[0]), D, 0, None)
+        else:
+            d = np.diff(p)
+            stride = int(d[0])
+            if (d == stride).all() and stride > 0 and stride % es == 0 and stride // es >= D:
+                c = (int(p[0]), stride // es, 0, None)
+            else:
+                if (p % es).any():
+                    raise ArgumentError("column pointers must be aligned to the element size")
+                vec = not (p % 16).any() and (D * es) % 16 == 0
+                ld = D if vec or (D * es) % 16 else D + 1
+                ptrs = torch.from_numpy(p).to(self.example().device)
+                c = (ptrs.data_ptr(), ld, 1, ptrs)  # the tensor keeps the array alive
+        self.__dict__["_desc_cache"] = c
+        return c
+
     def device_table(self) -> tuple[int, int]:
-        """``(table, cols_per_page)`` for an et_lookup_desc / et_update_desc: the first
-        column's address and 0 for a contiguous table (the default)."""
-        return self.columnpointer(1), 0
+        """``(table, cols_per_page)`` for an et_lookup_desc / et_update_desc (see the
+        class docstring)."""
+        t, _, cpp, _ = self._describe()
+        return t, cpp
+
+    @property
+    def ld(self) -> int:
+        """``ld_table`` of the descriptor (elements between columns)."""
+        return self._describe()[1]
 
     @property
     def dtype(self):

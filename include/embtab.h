@@ -138,7 +138,12 @@ typedef struct et_lookup_desc {
                             SplitEmbedding, src/split.jl:3-86): `table` is a device array of
                             page pointers, column r (1-based) lives in page (r-1)/cols_per_page
                             at column (r-1)%cols_per_page, ld_table apart within a page;
-                            every page pointer must be 16-byte aligned (hipMalloc gives 256) */
+                            every page pointer must be 16-byte aligned (hipMalloc gives 256)
+                            when ld_table * elsize is a multiple of 16 bytes; otherwise the
+                            generic (element-aligned) kernels run.  cols_per_page = 1 is a
+                            COLUMN-POINTER table — `table` holds one pointer per column, any
+                            layout — the form any `columnpointer`-only table type takes
+                            (README.md:288-307); ld_table is then only that alignment switch */
 } et_lookup_desc;
 
 /* Fused lookup + concat (PreallocationStrategy):
