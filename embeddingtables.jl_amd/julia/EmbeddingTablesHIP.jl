@@ -99,6 +99,14 @@ function upload(A::Array{T,N}) where {T,N}
           D.ptr, A, sizeof(A), 1) == 0 || error("hipMemcpy failed")
     return D
 end
+# Device array -> host array (hipMemcpyDeviceToHost, after the stream's work).
+function download(A::HipArray{T,N}) where {T,N}
+    H = Array{T,N}(undef, size(A))
+    ccall((:hipStreamSynchronize, libhip), Cint, (Ptr{Cvoid},), stream())
+    ccall((:hipMemcpy, libhip), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Csize_t, Cint),
+          H, A.ptr, sizeof(H), 2) == 0 || error("hipMemcpy failed")
+    return H
+end
 
 #####
 ##### The table type (AbstractEmbeddingTable contract, README.md:288-307)
@@ -148,7 +156,44 @@ example(A::HipSplitEmbedding) = first(A.pages)
 _device_table(A::HipEmbedding) = (Ptr{Cvoid}(A.data.ptr), leading(A.data), 0)
 _device_table(A::HipSplitEmbedding) = (Ptr{Cvoid}(A.pagetable.ptr), A.matrixsize[1],
                                        A.matrixsize[2])
-const HipTable{S,T} = Union{HipEmbedding{S,T},HipSplitEmbedding{S,T}}
+# Any other table type that implements only the plug-in contract (size / columnpointer
+# / example, README.md:288-307 — e.g. test/constructors.jl's DummyEmbedding over a
+# HipMatrix), with its columns in device memory: wrap it as DeviceColumns(table) (the
+# wrapper forwards the contract, so the reference's generic code still sees the user
+# type's behaviour; it only routes the hot methods here).  Equally spaced columns give a
+# contiguous descriptor; anything else a device array of column pointers, one column per
+# "page" (cols_per_page = 1).  With 16-byte aligned pointers and rows the vector kernels
+# run; otherwise ld_table is set to a non-16-byte spacing, which selects the
+# element-aligned kernels (include/embtab.h).
+mutable struct DeviceColumns{S,T,A<:AbstractEmbeddingTable{S,T}} <: AbstractEmbeddingTable{S,T}
+    table::A
+    desc::Any  # (table pointer, ld, cols_per_page, pointer array or nothing), built once
+end
+DeviceColumns(A::AbstractEmbeddingTable{S,T}) where {S,T} =
+    DeviceColumns{S,T,typeof(A)}(A, nothing)
+Base.size(A::DeviceColumns) = size(A.table)
+Base.getindex(A::DeviceColumns, i::Int) = A.table[i]
+Base.setindex!(A::DeviceColumns, v, i::Int) = (A.table[i] = v)
+columnpointer(A::DeviceColumns, i::Integer) = columnpointer(A.table, i)
+example(A::DeviceColumns) = example(A.table)
+function _device_table(A::DeviceColumns{S,T}) where {S,T}
+    if A.desc === nothing
+        D, R = size(A)
+        p = UInt64[UInt64(columnpointer(A.table, i)) for i in 1:R]
+        d = diff(p)
+        A.desc = if R == 1 || (all(==(d[1]), d) && d[1] % sizeof(T) == 0 &&
+                               d[1] ÷ sizeof(T) >= D)
+            (Ptr{Cvoid}(p[1]), R == 1 ? D : Int(d[1] ÷ sizeof(T)), 0, nothing)
+        else
+            vec = all(x -> x % 16 == 0, p) && (D * sizeof(T)) % 16 == 0
+            ld = vec || (D * sizeof(T)) % 16 != 0 ? D : D + 1
+            dp = upload(p)  # kept alive by the wrapper
+            (Ptr{Cvoid}(dp.ptr), ld, 1, dp)
+        end
+    end
+    return A.desc[1:3]
+end
+const HipTable{S,T} = Union{HipEmbedding{S,T},HipSplitEmbedding{S,T},DeviceColumns{S,T}}
 
 # Preallocation gradients are row blocks of one big matrix: a view's leading dimension.
 _ptr_ld(A::HipMatrix) = (Ptr{Cvoid}(A.ptr), leading(A))
@@ -198,8 +243,10 @@ struct LookupDesc
     cols_per_page::Int64
 end
 
-# A paged table's single-table lookup! goes through the descriptor entry point.
-function lookup!(dst, A::HipSplitEmbedding{S,T}, I::Union{HipVector{Int},HipMatrix{Int}}) where {S,T}
+# A paged or column-pointer table's single-table lookup! goes through the descriptor
+# entry point.
+function lookup!(dst, A::Union{HipSplitEmbedding{S,T},DeviceColumns{S,T}},
+                 I::Union{HipVector{Int},HipMatrix{Int}}) where {S,T}
     p, ld = _ptr_ld(dst)
     tp, ldt, cpp = _device_table(A)
     pool = ndims(I) == 1 ? 1 : size(I, 1)
@@ -295,12 +342,20 @@ function update!(opt::Flux.Descent, table::HipTable{S,T}, grad::SparseEmbeddingU
     return nothing
 end
 
+# src/sparseupdate.jl:199-238: index all tables, telemetry_cb(), update all tables.
+# One device pipeline per (path, eltype) group, split at the same boundary
+# (ET_FLAG_SGD_INDEX_ONLY, then ET_FLAG_SGD_APPLY_ONLY from the same workspace);
+# telemetry_cb runs once the index phase is enqueued.  With fill_indexers (default),
+# indexers[i] receives table i's Indexer from the reference's own index! on a host copy
+# of the indices, on the CPU while the GPU runs the index phase.
+const WORKSPACES = Dict{Int,Any}()
 function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  grads::AbstractVector{<:SparseEmbeddingUpdate},
                  indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
-                 telemetry_cb = Returns(nothing), kw...) where {Nontemporal}
-    telemetry_cb()
+                 telemetry_cb = Returns(nothing), fill_indexers::Bool = true,
+                 kw...) where {Nontemporal}
     nt = Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)
+    calls = []
     for fused in (true, false), T in (Float32, Float64, Float16)
         sel = [i for i in eachindex(tables) if _fused(tables[i]) == fused &&
                                                eltype(tables[i]) === T]
@@ -308,13 +363,127 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
         # the multi-table generic path sees opt.eta as Float64 (src/sparseupdate.jl:232)
         flags = nt | (fused ? UInt32(0) : ET_FLAG_SGD_UNFUSED | ET_FLAG_SGD_F64_ALPHA)
         for chunk in Iterators.partition(sel, 32)
-            _sparse_sgd(T, [_update_desc(tables[i], grads[i]) for i in chunk],
-                        Float64(opt.eta), flags)
+            descs = [_update_desc(tables[i], grads[i]) for i in chunk]
+            nb = Ref{Int64}(0)
+            check(ccall((:et_sgd_workspace_size, libembtab), Cint,
+                        (Ptr{UpdateDesc}, Int32, Ref{Int64}), descs, length(descs), nb))
+            k = length(calls)
+            ws = get(WORKSPACES, k, nothing)
+            if ws === nothing || length(ws) < nb[]
+                ws = HipArray{UInt8}(undef, nb[])
+                WORKSPACES[k] = ws
+            end
+            push!(calls, (T, descs, flags, ws))
         end
     end
+    run(phase) = for (T, descs, flags, ws) in calls
+        check(ccall((:et_sparse_sgd, libembtab), Cint,
+                    (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                    et_dtype(T), descs, length(descs), Float64(opt.eta), flags | phase, ws.ptr,
+                    length(ws), stream()))
+    end
+    run(ET_FLAG_SGD_INDEX_ONLY)
+    if fill_indexers
+        for i in eachindex(indexers, grads)
+            EmbeddingTables.index!(indexers[i], download(grads[i].indices), size(tables[i], 2))
+        end
+    end
+    telemetry_cb()
+    run(ET_FLAG_SGD_APPLY_ONLY)
     return nothing
 end
 
-export HipEmbedding, HipSplitEmbedding, HipArray, HipVector, HipMatrix, EmbtabError
+#####
+##### Sharded Preallocation maplookup over the GPUs of a node (BASELINE config 5):
+##### one Julia process per GPU, RCCL over xGMI (include/embtab.h, csrc/et_shard.cpp)
+#####
+
+struct ShardPiece
+    rank::Int32
+    table::Int32
+    f0::Int32
+    dim::Int32
+    col::Int64
+end
+
+const ET_PLAN_TABLEWISE, ET_PLAN_FEATUREWISE = Int32(0), Int32(1)
+const ET_EXCHANGE_ALLGATHER, ET_EXCHANGE_ALLTOALL = Int32(0), Int32(1)
+
+function shard_plan(dims::Vector{Int32}, world; mode = ET_PLAN_TABLEWISE, prependrows = 0,
+                    sizes = nothing, granule = 32, elsize = 4)
+    n = Ref{Int32}(0)
+    sz = sizes === nothing ? C_NULL : Int64.(sizes)
+    args() = (mode, Int32(length(dims)), dims, sz, Int32(world), Int64(prependrows),
+              Int32(granule), Int32(elsize))
+    check(ccall((:et_shard_plan, libembtab), Cint,
+                (Int32, Int32, Ptr{Int32}, Ptr{Int64}, Int32, Int64, Int32, Int32,
+                 Ptr{ShardPiece}, Int32, Ref{Int32}), args()..., C_NULL, 0, n))
+    out = Vector{ShardPiece}(undef, n[])
+    check(ccall((:et_shard_plan, libembtab), Cint,
+                (Int32, Int32, Ptr{Int32}, Ptr{Int64}, Int32, Int64, Int32, Int32,
+                 Ptr{ShardPiece}, Int32, Ref{Int32}), args()..., out, n[], n))
+    return out
+end
+
+# Rank 0: comm_id(); the host broadcasts the 128 bytes (MPI.Bcast!, a TCP store, ...);
+# every rank: comm_init(id, world, rank) on its own GPU.
+function comm_id()
+    id = Vector{UInt8}(undef, 128)
+    check(ccall((:et_comm_unique_id, libembtab), Cint, (Ptr{UInt8},), id))
+    return id
+end
+function comm_init(id::Vector{UInt8}, world, rank)
+    c = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:et_comm_init, libembtab), Cint, (Ref{Ptr{Cvoid}}, Int32, Ptr{UInt8}, Int32),
+                c, world, id, rank))
+    return c[]
+end
+
+mutable struct ShardedPreallocation
+    handle::Ptr{Cvoid}
+    workspace::HipVector{UInt8}
+    rank::Int
+    batch_range::UnitRange{Int}
+end
+
+function ShardedPreallocation(comm, plan::Vector{ShardPiece}, world, rank, ::Type{T},
+                              prependrows, ld_dst, batch; chunks = 4,
+                              exchange = ET_EXCHANGE_ALLGATHER) where {T}
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:et_sharded_create, libembtab), Cint,
+                (Ref{Ptr{Cvoid}}, Ptr{Cvoid}, Int32, Int32, Cint, Ptr{ShardPiece}, Int32, Int64,
+                 Int64, Int64, Int32, Int32),
+                h, comm, world, rank, et_dtype(T), plan, length(plan), prependrows, ld_dst,
+                batch, chunks, exchange))
+    ld, ws, lo, hi = Ref{Int64}(0), Ref{Int64}(0), Ref{Int64}(0), Ref{Int64}(0)
+    check(ccall((:et_sharded_info, libembtab), Cint,
+                (Ptr{Cvoid}, Ref{Int64}, Ref{Int64}, Ref{Int64}, Ref{Int64}), h[], ld, ws, lo, hi))
+    S = ShardedPreallocation(h[], HipArray{UInt8}(undef, ws[]), rank, (lo[] + 1):hi[])
+    finalizer(s -> ccall((:et_sharded_destroy, libembtab), Cint, (Ptr{Cvoid},), s.handle), S)
+    return S
+end
+
+# maplookup!(PreallocationStrategy(k), dst, tables, I) with this rank's pieces: `tables`
+# and `I` are the tables of this rank's plan entries, in plan order (whole tables for
+# the table-wise plan).
+function maplookup!(S::ShardedPreallocation, dst::HipMatrix{T}, tables::Vector{<:HipTable},
+                    I0) where {T}
+    I = EmbeddingTables.colwrap(I0)
+    descs = Vector{LookupDesc}(undef, length(tables))
+    for (t, (A, i)) in enumerate(zip(tables, I))
+        pool = ndims(i) == 1 ? 1 : size(i, 1)
+        tp, ldt, cpp = _device_table(A)
+        descs[t] = LookupDesc(tp, ldt, size(A, 2), size(A, 1), pool, pointer(i), pool, 0, cpp)
+    end
+    check(ccall((:et_sharded_maplookup, libembtab), Cint,
+                (Ptr{Cvoid}, Ptr{LookupDesc}, Int32, Ptr{Cvoid}, Int64, Ptr{Cvoid}, Int64, UInt32,
+                 Ptr{Cvoid}),
+                S.handle, descs, length(descs), dst.ptr, leading(dst), S.workspace.ptr,
+                length(S.workspace), ET_FLAG_NONTEMPORAL, stream()))
+    return dst
+end
+
+export HipEmbedding, HipSplitEmbedding, HipArray, HipVector, HipMatrix, EmbtabError,
+    DeviceColumns, ShardedPreallocation, shard_plan, comm_id, comm_init
 
 end # module
