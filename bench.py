@@ -427,7 +427,7 @@ def main():
 
     import embtab as et
     from embtab import _lib
-    from embtab.sharding import ShardedMapLookup, ShardPlan, piece_table
+    from embtab.sharding import ShardedMapLookup, ShardPlan, compact_piece_table
 
     if args.rows:
         CRITEO_KAGGLE_ROWS[:] = [args.rows] * len(CRITEO_KAGGLE_ROWS)
@@ -461,11 +461,17 @@ def main():
         plan = (ShardPlan.featurewise(dims, world) if args.plan == "featurewise"
                 else ShardPlan.tablewise(dims, world))
         mine = plan.tables_of(rank)
-        full = dict(zip(mine, make_tables(et, L, mine, device)))
-        fidx = dict(zip(mine, make_indices(L, mine, B, device)))
         pieces = plan.pieces[rank]
-        tables = [piece_table(full[p.table], p) for p in pieces]
+        tables = []
+        for t in mine:  # only the owned tables / feature slices stay resident
+            (full_t,) = make_tables(et, L, [t], device)
+            tables += [(k, compact_piece_table(full_t, p)) for k, p in enumerate(pieces)
+                       if p.table == t]
+            del full_t
+        tables = [tb for _, tb in sorted(tables, key=lambda x: x[0])]
+        fidx = dict(zip(mine, make_indices(L, mine, B, device)))
         idx = [fidx[p.table] for p in pieces]
+        torch.cuda.empty_cache()
         local_dims = [p.dim for p in pieces]
         shard = ShardedMapLookup(plan, rank, world, B, torch.float32, device,
                                  exchange="allgather", chunks=args.chunks)
@@ -604,6 +610,15 @@ def main():
     if sharded:
         result["lookup_only_ms"] = kernel_ms
         result["slab_cols"] = plan.slab_ld
+        # what every rank holds: its tables (or feature slices) only
+        mem = {"rank": rank, "tables": mine, "pieces": [(p.table, p.f0, p.dim) for p in pieces],
+               "table_bytes": sum(tb.data.numel() * tb.data.element_size() for tb in tables)}
+        every = [None] * world
+        if world > 1:
+            dist.all_gather_object(every, mem)
+        else:
+            every = [mem]
+        result["per_rank"] = every
         if world > 1 and not args.no_alltoall:
             try:  # an extra measurement: never lose the main line to it
                 result["alltoall"] = bench_alltoall(plan, rank, world, B, device, tables, idx,

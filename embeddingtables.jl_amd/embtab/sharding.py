@@ -170,6 +170,21 @@ def piece_table(full, piece: Piece):
     return SimpleEmbedding(view, Static(piece.dim) if fused_update_path(full) else Dynamic)
 
 
+def compact_piece_table(full, piece: Piece):
+    """``piece`` of a full table as its OWN compact ``(R, dim)`` table (ld = dim): a rank
+    that owns a feature slice stores only that slice (feature-wise plans).  Whole-table
+    pieces return the table itself.  Same update dispatch as the parent."""
+    from .tables import Dynamic, SimpleEmbedding, Static, fused_update_path
+
+    D = full.size()[0]
+    if piece.f0 == 0 and piece.dim == D:
+        return full
+    if not isinstance(full, SimpleEmbedding):
+        raise NotImplementedError("feature-sharding needs SimpleEmbedding tables")
+    data = full.data[:, piece.f0:piece.f0 + piece.dim].contiguous()
+    return SimpleEmbedding(data, Static(piece.dim) if fused_update_path(full) else Dynamic)
+
+
 class ShardedMapLookup:
     """``maplookup!(PreallocationStrategy(k), dst, tables, I)`` over the ranks of
     ``group`` (RCCL on ROCm; gloo for CPU rehearsal).

@@ -143,3 +143,22 @@ def test_sharded_prealloc_gloo(world):
     n = world * 3 * 3
     res = [q.get(timeout=5) for _ in range(n)]
     assert len(res) == n and all(r[-1] for r in res), [r for r in res if not r[-1]]
+
+
+def test_compact_piece_tables_hold_only_the_slice():
+    """Feature-wise ranks keep their slice as its own (R, dim) table (ld = dim), not a
+    view of the full table: values equal the slice, memory is the slice's."""
+    import torch
+
+    import embtab as et
+    from embtab.sharding import Piece, compact_piece_table
+
+    full = et.SimpleEmbedding(torch.arange(40 * 128, dtype=torch.float32).view(40, 128),
+                              et.Static(128))
+    p = Piece(3, 32, 64, 7)
+    c = compact_piece_table(full, p)
+    assert c.data.shape == (40, 64) and c.ld == 64 and c.data.is_contiguous()
+    assert torch.equal(c.data, full.data[:, 32:96])
+    assert c.data.untyped_storage().nbytes() == 40 * 64 * 4
+    assert c.lookup_type == et.Static(64)
+    assert compact_piece_table(full, Piece(3, 0, 128, 7)) is full
