@@ -411,6 +411,41 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
                 (occ * DIM * 4 + 2 * U * DIM * 4 + occ * 8) / (upd_ms * 1e-3) / 1e9}
 
 
+def bench_config3_fp16(et, L, tids, idx, device, steps, warmup, batch):
+    """SURVEY.md §8f rank 4 / north_star "fp32/fp16 embedding columns": the config-3
+    workload with Float16 tables (same seeds, 8.6 GB), in the reference's Float16
+    arithmetic (every add rounded to half, as Julia's) and with fp32 accumulation
+    (ET_FLAG_F16_FP32_ACC, one rounding).  An extra line, never the headline."""
+    import torch
+    from embtab import _lib
+
+    stream = torch.cuda.current_stream(device)
+    tabs = []
+    for t in tids:
+        R = CRITEO_KAGGLE_ROWS[t]
+        data = torch.empty((R, DIM), dtype=torch.float16, device=device)
+        _lib.check(L.et_fill_uniform(_lib.ET_F16, data.data_ptr(), data.numel(), TABLE_SEED + t, 0,
+                                     0.0, 1.0, stream.cuda_stream))
+        tabs.append(et.SimpleEmbedding(data, et.Static(DIM)))
+    dst = torch.empty((batch, DIM * len(tabs)), dtype=torch.float16, device=device)
+    strat = et.PreallocationStrategy(0)
+    out = {"workload": "config 3 with Float16 tables (26 x 128, pool 20, B = 65536)"}
+    rows = [CRITEO_KAGGLE_ROWS[t] for t in tids]
+    hbm = hbm_compulsory_bytes(batch, POOL, [DIM] * len(tabs), rows, es=2)
+    alg = algorithmic_bytes(batch, POOL, [DIM] * len(tabs), es=2)
+    for key, acc in (("julia_f16_arith", False), ("fp32_accumulate", True)):
+        plan = et.PreallocationPlan(strat, dst, tabs, idx, True, acc)
+        ms = _timed(plan, steps, warmup, stream)
+        out[key] = {"kernel_ms": ms, "lookups_per_s": batch * len(tabs) * POOL / (ms * 1e-3),
+                    "hbm_compulsory_GBs": hbm / (ms * 1e-3) / 1e9,
+                    "hbm_frac": hbm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "algorithmic_GBs": alg / (ms * 1e-3) / 1e9}
+    out["hbm_compulsory_bytes_per_launch"] = hbm
+    del tabs, dst
+    torch.cuda.empty_cache()
+    return out
+
+
 def load_traffic():
     path = os.path.join(REPO, "profiles", "traffic_r01.json")
     try:
@@ -640,6 +675,7 @@ def main():
                                        "lookups_per_s": lookups_per_step / (ms16 * 1e-3)}
         del dst16
     if world == 1 and not args.no_extra:
+        result["config3_fp16"] = bench_config3_fp16(et, L, mine, idx, device, 20, 3, B)
         result["config2_gather"] = bench_config2(et, L, device, 320, 2)
         result["config4_zipf_update"] = bench_config4(et, tables, mine, device, 10, 2, B)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

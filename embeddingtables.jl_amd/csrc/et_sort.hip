@@ -238,11 +238,15 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restri
         hs[(uint64_t)d * tiles + tl] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
-// Stable scatter of one tile: 32 rounds of 256 keys in input order; a key's rank among
-// equal digits is (keys of this digit in earlier rounds) + (lower waves of this round)
-// + (lower lanes of its wave, found with one ballot per digit bit).  (Measured faster
-// on gfx950 than barrier-free wave-private ranking and than LDS-staged coalesced
-// write-out variants, which lose occupancy)
+// Stable scatter of one tile (8192 keys).  Full tiles of a 16-byte aligned segment are
+// staged in LDS by LDS-DMA (74 KB, 2 workgroups per CU), sorted by digit in LDS and
+// written out in bucket runs (below).  The tail tile takes the round path: 32 rounds of
+// 256 keys in input order; a key's rank among equal digits is (keys of this digit in
+// earlier rounds) + (lower waves of this round) + (lower lanes of its wave, found with
+// one ballot per digit bit).  Config-4 update, passes in order (8-bit over the 6 largest
+// tables' 7.9 M pairs, 9-bit over 22 M, 9-bit over 34 M; rocprofv3 kernel trace): 49 /
+// 143 / 211 us staged against 141 / 359 / 231 us with the round path alone — its
+// scattered 4-byte stores (one L2 write request each) were its bound.
 template <int BITS>
 __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
@@ -251,27 +255,126 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
     constexpr int NB = 1 << BITS;
     __shared__ uint32_t base_of[NB];
     __shared__ uint32_t wcnt[4][NB];
+    // the whole tile's keys and values, staged by LDS-DMA (full, 16-byte aligned tiles)
+    __shared__ uint32_t skey[kRsTile];
+    __shared__ uint32_t sval[kRsTile];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int k = rs_segment(p, blockIdx.x);
     const uint32_t tl = blockIdx.x - p.tile_off[k], tiles = p.tile_off[k + 1] - p.tile_off[k];
     const uint32_t n = p.n[k], kb = p.key_base[k], cap = p.key_cap[k], sh = p.shift[k];
     const uint32_t e0 = p.elem0[k], pb = p.pos_base[k];
     const uint32_t* hs = hist_scanned + (uint64_t)NB * p.tile_off[k];
+    const uint32_t base = tl * kRsTile;
+    // Full tiles of a 16-byte aligned segment: every key and value of the tile is
+    // requested at once (16 global_load_lds_dwordx4 per wave, no VGPRs), so the tile
+    // pays one memory latency instead of one per round of 256 keys; the tail tile
+    // keeps the register path with a one-round prefetch.
+    const bool staged = base + kRsTile <= n && ((e0 & 3u) == 0);  // workgroup-uniform
+    if (staged) {
+#pragma unroll
+        for (int j = 0; j < kRsItems / 4; ++j) {
+            const int c = (j * 4 + wave) * 256;  // this wave-instruction's 256 keys (1 KiB)
+            __builtin_amdgcn_global_load_lds(kin + e0 + base + c + lane * 4, &skey[c], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(vin + e0 + base + c + lane * 4, &sval[c], 16, 0, 0);
+        }
+    }
     for (int d = threadIdx.x; d < NB; d += kRsThreads) {
         base_of[d] = hs[(uint64_t)d * tiles + tl] + pb;
         wcnt[0][d] = wcnt[1][d] = wcnt[2][d] = wcnt[3][d] = 0;
     }
-    __syncthreads();
+    __syncthreads();  // (with LDS-DMA in flight this waits vmcnt(0): the tile has landed)
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t base = tl * kRsTile;
-    // keys / values of the next round are loaded while this round is ranked
+    // register path: keys / values of the next round are loaded while this round is ranked
     uint32_t key_n = 0, val_n = 0;
-    {
+    if (!staged) {
         const uint32_t i = base + threadIdx.x;
         if (i < n) {
             key_n = kin[e0 + i];
             val_n = vin[e0 + i];
         }
+    }
+    if (staged) {
+        // Staged tile, sorted in LDS, written out in bucket runs.  Wave q owns the
+        // tile's keys [q * 2048, (q + 1) * 2048) (input order = wave-major):
+        //  1. each wave counts its keys' digits in its own LDS row (wcnt[q]);
+        //  2. tile-local offsets: dpre[d] = keys of smaller digits in the tile, and row
+        //     (q, d) starts at dpre[d] + keys of digit d in waves < q;
+        //  3. each wave walks its keys in order: a key's rank among equal digits within a
+        //     64-key round comes from the ballots, the running offset from its wave's
+        //     row, which only that wave updates (LDS ops of one wave run in program
+        //     order) — stable, no barrier per round; keys, values and tile-local sorted
+        //     positions stay in registers;
+        //  4. after a barrier every key and value is written to its sorted slot of the
+        //     LDS tile, and after another the tile is written out slot by slot: digit d's
+        //     run (about 16 keys at 512 buckets) lands at consecutive global positions, so
+        //     a store instruction touches a few cache lines instead of 64 (one L2 write
+        //     request per scattered 4-byte key was this kernel's bound).
+        constexpr int kPer = kRsTile / 4;
+        constexpr int kRounds = kPer / 64;
+        __shared__ uint32_t dpre[NB];
+        const uint32_t* wk = skey + wave * kPer;
+        const uint32_t* wv = sval + wave * kPer;
+        for (int rr = 0; rr < kPer; rr += 64)
+            atomicAdd(&wcnt[wave][rs_digit<NB>(wk[rr + lane], kb, cap, sh)], 1u);
+        __syncthreads();
+        {
+            // exclusive scan of the tile's digit totals (NB / 256 digits per thread)
+            constexpr int DPT = NB / kRsThreads;
+            uint32_t tot[DPT], sum = 0;
+#pragma unroll
+            for (int q = 0; q < DPT; ++q) {
+                const int d = threadIdx.x * DPT + q;
+                tot[q] = wcnt[0][d] + wcnt[1][d] + wcnt[2][d] + wcnt[3][d];
+                sum += tot[q];
+            }
+            __shared__ uint32_t lds4[4];
+            uint32_t total;
+            uint32_t run = block_inclusive_scan_256(sum, lds4, &total) - sum;
+#pragma unroll
+            for (int q = 0; q < DPT; ++q) {
+                const int d = threadIdx.x * DPT + q;
+                dpre[d] = run;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t c = wcnt[w][d];
+                    wcnt[w][d] = run;
+                    run += c;
+                }
+            }
+        }
+        __syncthreads();
+        uint32_t rk[kRounds], rv[kRounds], rl[kRounds];
+#pragma unroll
+        for (int q = 0; q < kRounds; ++q) {
+            const uint32_t key = wk[q * 64 + lane];
+            const uint32_t d = rs_digit<NB>(key, kb, cap, sh);
+            uint64_t same = ~0ull;
+#pragma unroll
+            for (int b = 0; b < BITS; ++b) {
+                const uint64_t ones = __ballot((d >> b) & 1u);
+                same &= ((d >> b) & 1u) ? ones : ~ones;
+            }
+            const uint32_t rank = __popcll(same & lt_mask);
+            rl[q] = wcnt[wave][d] + rank;
+            if (rank == 0) wcnt[wave][d] += (uint32_t)__popcll(same);  // after every lane's read
+            rk[q] = key;
+            rv[q] = wv[q * 64 + lane];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kRounds; ++q) {
+            skey[rl[q]] = rk[q];
+            sval[rl[q]] = rv[q];
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < kRsTile; j += kRsThreads) {
+            const uint32_t key = skey[j];
+            const uint32_t d = rs_digit<NB>(key, kb, cap, sh);
+            const uint32_t pos = base_of[d] + (uint32_t)j - dpre[d];
+            kout[pos] = key;
+            vout[pos] = sval[j];
+        }
+        return;
     }
     for (int r = 0; r < kRsItems; ++r) {
         const uint32_t i = base + r * kRsThreads + threadIdx.x;

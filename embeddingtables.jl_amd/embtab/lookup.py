@@ -198,7 +198,7 @@ def maplookup(*args, **kw):
 
 
 def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal: bool = True,
-               worksize_div: int = 8):
+               worksize_div: int = 8, f16_fp32_acc: bool = False):
     """``maplookup!(strategy, dst, tables, I)``.
 
     Default / SimpleParallel: one launch per table.  Preallocation: ONE fused launch
@@ -213,7 +213,7 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
 
     if not tables:
         return dst
-    return PreallocationPlan(strategy, dst, tables, Is, nontemporal)()
+    return PreallocationPlan(strategy, dst, tables, Is, nontemporal, f16_fp32_acc)()
 
 
 class PreallocationPlan:
@@ -222,7 +222,8 @@ class PreallocationPlan:
     call is one call into the library (no per-table Python work) — for serving loops
     that refill the index buffers in place, and for the sharded step's chunks."""
 
-    def __init__(self, strategy: PreallocationStrategy, dst, tables, I, nontemporal=True):
+    def __init__(self, strategy: PreallocationStrategy, dst, tables, I, nontemporal=True,
+                 f16_fp32_acc: bool = False):
         tables = list(tables)
         Is = colwrap(I)
         if len(Is) != len(tables):
@@ -260,6 +261,8 @@ class PreallocationPlan:
         self._n = len(tables)
         self._B = B
         self._flags = _lib.ET_FLAG_NONTEMPORAL if nontemporal else 0
+        if f16_fp32_acc:  # Float16 tables: fp32 sums, one rounding (not Julia's Float16 ops)
+            self._flags |= _lib.ET_FLAG_F16_FP32_ACC
         self._src = _lib.TORCH_TO_ET[dtype]
         self._dst_t = _lib.et_dtype(dst)
         self._dst = dst
