@@ -447,12 +447,20 @@ def bench_config3_fp16(et, L, tids, idx, device, steps, warmup, batch):
 
 
 def load_traffic():
-    path = os.path.join(REPO, "profiles", "traffic_r01.json")
-    try:
-        with open(path) as f:
-            return json.load(f)
-    except (OSError, ValueError):
-        return None
+    """The latest committed PMC traffic summary of the headline kernel
+    (profiles/traffic_rNN.json, written by tools/traffic.py)."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "traffic_r*.json")),
+                       reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+            doc["file"] = os.path.relpath(path, REPO)
+            return doc
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def main():
@@ -628,6 +636,7 @@ def main():
             "algorithmic_GBs": algorithmic_GBs,
             "algorithmic_frac": algorithmic_GBs / HBM_PEAK_GBS,
             "traffic": traffic_bytes,
+            "traffic_source": traffic.get("file") if traffic_bytes else None,
             # fabric-side bytes (PMC, per launch) over the same launch time: how close the
             # memory system itself runs to the HBM peak (cache-resident tables make the
             # algorithmic rate exceed it)

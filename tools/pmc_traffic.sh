@@ -10,5 +10,5 @@ cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p "$OUT"
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
   tag=$(echo "$grp" | tr ' ' '_')
-  timeout -k 10 300 rocprofv3 --pmc $grp -d "$OUT/$tag" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/$tag.log" 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc $grp -d "$OUT/$tag" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/$tag.log" 2>&1
 done
