@@ -688,10 +688,24 @@ def main():
         result["config2_gather"] = bench_config2(et, L, device, 320, 2)
         result["config4_zipf_update"] = bench_config4(et, tables, mine, device, 10, 2, B)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        threads = args.cpu_threads or (os.cpu_count() or 1)
         gpu_out = None if args.no_check else dst.cpu().numpy()
-        result["cpu_baseline"] = cpu_baseline(gpu_out, idx, B, args.cpu_seconds, threads,
-                                              not args.no_check)
+        if args.cpu_threads:
+            result["cpu_baseline"] = cpu_baseline(gpu_out, idx, B, args.cpu_seconds,
+                                                  args.cpu_threads, not args.no_check)
+        else:
+            # every host core, and the CPUs the job's cgroup may actually use (the GPU
+            # box caps a job at 16 CPUs of its 256: cpu.max); the faster run is the
+            # baseline, both are reported
+            cores, _, quota = host_cpus()
+            widths = [cores] + ([int(quota)] if quota and int(quota) < cores else [])
+            runs = [cpu_baseline(gpu_out, idx, B, args.cpu_seconds if k == 0 else
+                                 max(2.0, args.cpu_seconds / 3), w, not args.no_check and k == 0)
+                    for k, w in enumerate(widths)]
+            best = max(runs, key=lambda r: r["value"])
+            best["widths_tried"] = {str(r["threads"]): r["value"] for r in runs}
+            if best is not runs[0]:
+                best["gpu_output_bit_identical"] = runs[0]["gpu_output_bit_identical"]
+            result["cpu_baseline"] = best
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
