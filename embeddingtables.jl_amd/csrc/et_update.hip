@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, float* __restrict__ partials, int pdim,
-    uint32_t sent, float eta32, double eta64, uint32_t my_mask) {
+    uint32_t sent, float eta32, double eta64, uint32_t my_mask, int skip_singles) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -410,10 +410,23 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
         const uint64_t cl = ((uint64_t)it * 64u + lane) * nwaves + wid;
         const bool valid = cl < C;
         const ChunkRec r = recs[valid ? (uint32_t)cl : C - 1];
-        const uint32_t m_s0 = r.s0, m_s1 = r.s1, m_dst = r.dst;
-        const uint32_t m_key = valid ? r.key : sent;
+        uint32_t m_s0 = r.s0, m_s1 = r.s1, m_dst = r.dst;
+        uint32_t m_key = valid ? r.key : sent;
         const uint64_t left = ((uint64_t)C - wid + nwaves - 1) / nwaves - (uint64_t)it * 64u;
-        const uint32_t nq = left < 64u ? (uint32_t)left : 64u;
+        uint32_t nq = left < 64u ? (uint32_t)left : 64u;
+        if (skip_singles) {
+            // the records this pass walks (not k_sgd_singles'), compacted to the front
+            const bool keep = valid && m_key != sent && !(m_dst == kApply && m_s1 - m_s0 == 1u);
+            const uint64_t bal = (uint64_t)__ballot(keep);
+            const int nk = __popcll(bal);
+            const int rk = __popcll(bal & ((1ull << lane) - 1ull));
+            const int to = (keep ? rk : nk + (lane - rk)) << 2;
+            m_s0 = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)m_s0);
+            m_s1 = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)m_s1);
+            m_dst = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)m_dst);
+            m_key = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(keep ? m_key : sent));
+            nq = (uint32_t)nk;
+        }
         for (uint32_t qq = 0; qq < nq; qq += GPW) {
             const uint32_t kkey = group_pick<GPW>(m_key, (int)qq, g);
             const uint32_t s0 = group_pick<GPW>(m_s0, (int)qq, g);
@@ -448,6 +461,123 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
                     if (sub + v * LPR < vpr)
                         pp[v * LPR] = u32x4{__float_as_uint(acc[v][0]), __float_as_uint(acc[v][1]),
                                             __float_as_uint(acc[v][2]), __float_as_uint(acc[v][3])};
+            }
+        }
+    }
+}
+
+// Single-occurrence columns (70% of the chunks on the config-4 batch, 1.34 M of 2.0 M):
+// in k_sgd_chunks each is a chain of dependent loads (record -> occurrence id -> Δ
+// column and table column -> store) walked one chunk per lane group at a time, so the
+// pass waits on memory latency.  Here a wave takes the same 64 records at a time, keeps
+// the singles (compacted to the front with a lane permute), and each lane group updates
+// K of them together: K occurrence-id loads, then K Δ-column and K table-column loads in
+// flight, then K stores.  Same arithmetic as the chunk path (acc = +0 + Δ, then the
+// update), bit for bit.
+// Per-table fields the singles kernel reads with a per-lane table index, staged in LDS
+// (indexing the kernel-argument descriptors per lane would loop over the distinct
+// tables of the wave).
+struct SingleTab {
+    uint64_t table, delta;
+    uint32_t ld_table, ld_delta, pool, vpr, row_off, occ_off;
+    uint64_t cols_per_page;
+};
+
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_singles(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ vals,
+    const ChunkRec* __restrict__ recs, const uint32_t* __restrict__ counters, uint32_t sent,
+    float eta32, double eta64, uint32_t my_mask) {
+    constexpr int VPR = D / 4;
+    constexpr int LPR = VPR < 64 ? VPR : 64;
+    constexpr int NV = VPR / LPR;
+    constexpr int GPW = 64 / LPR;
+    constexpr int K = NV >= 8 ? 1 : 8 / NV;  // singles per lane group at a time
+    __shared__ SingleTab tabs[ET_MAX_TABLES_PER_LAUNCH];
+    if (threadIdx.x < (unsigned)ntables) {
+        const et_update_desc& d = pack.d[threadIdx.x];
+        tabs[threadIdx.x] = SingleTab{(uint64_t)d.table, (uint64_t)d.delta, (uint32_t)d.ld_table,
+                                      (uint32_t)d.ld_delta, (uint32_t)d.pool, (uint32_t)(d.dim / 4),
+                                      pack.row_off[threadIdx.x], pack.occ_off[threadIdx.x],
+                                      (uint64_t)d.cols_per_page};
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / LPR, sub = lane % LPR;
+    const uint32_t C = counters[kCntC];
+    const uint32_t nwaves = gridDim.x * 4u;
+    const uint32_t wid = blockIdx.x * 4u + wave;
+    for (uint32_t it = 0; (uint64_t)it * 64u * nwaves + wid < C; ++it) {
+        // one record per lane: singles get their table-column and Δ-column addresses
+        const uint64_t cl = ((uint64_t)it * 64u + lane) * nwaves + wid;
+        bool single = false;
+        uint64_t wpa = 0, dpa = 0;
+        uint32_t vp = 0;
+        if (cl < C) {
+            const ChunkRec r = recs[(uint32_t)cl];
+            if (r.dst == kApply && r.s1 - r.s0 == 1u && r.key != sent) {
+                int t = 0;  // wave-uniform loop over the (scalar) prefix, no per-lane branch
+                for (int i = 1; i < ntables; ++i) t += r.key >= pack.row_off[i] ? 1 : 0;
+                if ((my_mask >> t) & 1u) {
+                    const SingleTab tb = tabs[t];
+                    const uint32_t bag = (vals[r.s0] - tb.occ_off) / tb.pool;
+                    wpa = (uint64_t)col_ptr<float>((const void*)tb.table, tb.ld_table,
+                                                   (int64_t)tb.cols_per_page, r.key - tb.row_off);
+                    dpa = tb.delta + (uint64_t)bag * tb.ld_delta * 4u;
+                    vp = tb.vpr;
+                    single = true;
+                }
+            }
+        }
+        const uint64_t bal = (uint64_t)__ballot(single);
+        const int ns = __popcll(bal);
+        if (ns == 0) continue;  // wave-uniform
+        const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+        const int to = (single ? rank : ns + (lane - rank)) << 2;  // singles first
+        const uint32_t wlo = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)wpa);
+        const uint32_t whi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(wpa >> 32));
+        const uint32_t dlo = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)dpa);
+        const uint32_t dhi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(dpa >> 32));
+        const uint32_t vpp = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)vp);
+        // wave-uniform trip count: the lane reads below take other groups' lanes, so every
+        // lane stays active through them
+        for (int base = 0; base < ns; base += GPW * K) {
+            const int q0 = base + g * K;
+            const int m = ns - q0 < K ? ns - q0 : K;  // <= 0: this group has none left
+            float* wp[K];
+            int vpr[K];
+            u32x4 x[K][NV], y[K][NV];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                int j = q0 + (k < m ? k : m - 1);
+                j = j < ns ? (j < 0 ? 0 : j) : ns - 1;
+                const uint64_t w64 = ((uint64_t)(uint32_t)__shfl((int)whi, j, 64) << 32) |
+                                     (uint32_t)__shfl((int)wlo, j, 64);
+                const uint64_t d64 = ((uint64_t)(uint32_t)__shfl((int)dhi, j, 64) << 32) |
+                                     (uint32_t)__shfl((int)dlo, j, 64);
+                wp[k] = reinterpret_cast<float*>(w64);
+                vpr[k] = __shfl((int)vpp, j, 64);
+                int vix[NV];
+                vec_index<LPR, NV>(sub, vpr[k], vix);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    y[k][v] = reinterpret_cast<const u32x4*>(d64)[vix[v]];
+                    x[k][v] = reinterpret_cast<const u32x4*>(w64)[vix[v]];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (k < m) {
+                    float acc[NV][4];
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        acc[v][0] = 0.0f + __uint_as_float(y[k][v].x);
+                        acc[v][1] = 0.0f + __uint_as_float(y[k][v].y);
+                        acc[v][2] = 0.0f + __uint_as_float(y[k][v].z);
+                        acc[v][3] = 0.0f + __uint_as_float(y[k][v].w);
+                    }
+                    apply_row<D, MODE, NT>(wp[k], x[k], acc, sub, vpr[k], eta32, eta64);
+                }
             }
         }
     }
@@ -1046,12 +1176,23 @@ struct VecGroups {
     }
 };
 
+// Single-occurrence columns through k_sgd_singles (ET_SGD_SINGLES=0 turns it off for
+// experiments).
+inline bool sgd_singles() {
+    static const bool v = [] {
+        const char* e = getenv("ET_SGD_SINGLES");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
                      const VecGroups& vg, bool any_generic, hipStream_t s,
                      const HotList& hl, unsigned grid) {
     if constexpr (__is_same(T, float)) {
+        const bool singles = sgd_singles();
         if (hl.n > 0 && w.hot_part) {
             hipLaunchKernelGGL(k_sgd_hot, dim3((unsigned)w.hot_nw, (unsigned)hl.n), dim3(256), 0, s,
                                pack, hl, w.hot_cnt, w.hot_slots, w.hot_part, w.hot_nw);
@@ -1065,7 +1206,11 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     case DD:                                                                                   \
         hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
                            ntables, gr.keys, gr.vals, w.recs, w.counters, w.partials, pdim,    \
-                           sent, eta_c, eta64, vg.mask[i]);                                    \
+                           sent, eta_c, eta64, vg.mask[i], singles ? 1 : 0);                   \
+        if (singles)                                                                           \
+            hipLaunchKernelGGL((k_sgd_singles<DD, MODE, NT>), dim3(grid), dim3(256), 0, s,     \
+                               pack, ntables, gr.vals, w.recs, w.counters, sent, eta_c, eta64, \
+                               vg.mask[i]);                                                    \
         hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,   \
                            ntables, gr.keys, w.seg_start, w.multi, w.counters, w.mlist,        \
                            w.partials, pdim, sent, eta_c, eta64, vg.mask[i]);                  \
