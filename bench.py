@@ -298,19 +298,22 @@ def bench_alltoall(plan, rank, world, B, device, tables, idx, steps, warmup):
     from embtab.sharding import ShardedMapLookup
 
     a2a = ShardedMapLookup(plan, rank, world, B, torch.float32, device, exchange="alltoall")
-    out = torch.empty((a2a.mine, plan.ld), dtype=torch.float32, device=device)
-    for _ in range(warmup):
-        a2a(tables, idx, out)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        a2a(tables, idx, out)
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                      device=device if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    try:
+        out = torch.empty((a2a.mine, plan.ld), dtype=torch.float32, device=device)
+        for _ in range(warmup):
+            a2a(tables, idx, out)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            a2a(tables, idx, out)
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    finally:
+        a2a.close()
     ms = 1e3 * float(el.item()) / steps
     return {"ms_per_step": ms, "value": B * len(plan.dims) * POOL / (ms * 1e-3),
             "unit": "lookups/s", "output": "batch slice per rank"}
@@ -633,7 +636,8 @@ def main():
                                  "by count (SURVEY.md §8e)")
                            + f" x{world} + "
                            f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-gather concat "
-                           f"({shard.chunks} pipelined batch chunks)",
+                           f"({shard.chunks} pipelined batch chunks; "
+                           f"{'C-ABI et_sharded_maplookup' if shard._native else 'torch.distributed exchange'})",
         },
         "bags_per_s": B * T * args.steps / elapsed,
         "samples_per_s": B * args.steps / elapsed,
@@ -725,6 +729,8 @@ def main():
             result["cpu_baseline"] = best
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if sharded:
+        shard.close()  # the native step's stream, events and RCCL communicator
     if world > 1:
         dist.destroy_process_group()
 

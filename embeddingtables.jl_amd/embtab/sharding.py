@@ -204,13 +204,27 @@ class ShardedMapLookup:
         self.chunks = max(1, min(chunks, batch)) if exchange != "alltoall" else 1
         self.dtype = dtype
         self._native = None
-        if native is None:  # the C-ABI step whenever the ranks are real GPU processes
+        auto = native is None
+        if auto:  # the C-ABI step whenever the ranks are real GPU processes
             native = (exchange != "p2p" and self.device.type == "cuda" and
                       (world == 1 or self._nccl_group()))
         if native:
-            self._native = NativeShardedStep(plan, rank, world, batch, dtype, self.device,
-                                             group, exchange, self.chunks,
-                                             rccl=world > 1 if rccl is None else rccl)
+            try:
+                self._native = NativeShardedStep(plan, rank, world, batch, dtype, self.device,
+                                                 group, exchange, self.chunks,
+                                                 rccl=world > 1 if rccl is None else rccl)
+            except _lib.EmbtabError as e:
+                if not auto:
+                    raise
+                # the auto choice falls back to the torch.distributed exchange (same
+                # plan, same kernels, same results) when the library's RCCL communicator
+                # cannot be made; an explicit native=True request raises instead
+                import warnings
+
+                warnings.warn(f"native sharded step unavailable ({e}); using the "
+                              "torch.distributed exchange")
+                self._native = None
+        if self._native is not None:
             self.launches = plan.assembly_launches()
             nat = self._native
             # the slab is the head of the native workspace (for lookup-only timing)

@@ -397,6 +397,38 @@ def test_native_sharded_step_rccl_world1(oracle, exchange, chunks):
             sm.close()
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float64])
+def test_native_sharded_step_other_types(oracle, dtype):
+    """The C-ABI sharded step exchanges bytes, so every element type goes through it:
+    Float16 (Julia Float16 sums), BFloat16 and Float64 tables, feature-wise plan with
+    prepended rows, 3 pipelined chunks, one-rank RCCL communicator."""
+    from embtab.sharding import ShardedMapLookup, ShardPlan, piece_table
+
+    rng = np.random.default_rng(5)
+    dims, rows, B, k = [64, 128, 32], [200, 3000, 50], 257, 3
+    raw = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
+    hidx = [rng.integers(1, r + 1, (B, 12)) for r in rows]
+    if dtype == torch.bfloat16:
+        hs = [oracle.f32_to_bf16(x) for x in raw]
+        full = [et.SimpleEmbedding(dev(h).view(torch.bfloat16), et.Static(h.shape[1])) for h in hs]
+    else:
+        hs = [x.astype(np.float16 if dtype == torch.float16 else np.float64) for x in raw]
+        full = [table(h) for h in hs]
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=k, bf16=dtype == torch.bfloat16)
+    plan = ShardPlan.featurewise(dims, 1, k, elsize=torch.empty((), dtype=dtype).element_size())
+    sm = ShardedMapLookup(plan, 0, 1, B, dtype, DEV, chunks=3, rccl=True)
+    try:
+        assert sm._native is not None
+        dst = torch.zeros((B, plan.ld), dtype=dtype, device=DEV)
+        ps = plan.pieces[0]
+        sm([piece_table(full[p.table], p) for p in ps], [dev(hidx[p.table]) for p in ps], dst)
+        torch.cuda.synchronize()
+        got = host(dst.view(torch.int16)).view(np.uint16) if dtype == torch.bfloat16 else host(dst)
+        assert bits_equal(got[:, k:], ref[:, k:])
+    finally:
+        sm.close()
+
+
 def test_allgather_concat_rccl_world1():
     """et_allgather_concat on a one-rank RCCL communicator: ncclAllGather + assembly."""
     import ctypes
