@@ -209,6 +209,7 @@ class ShardedMapLookup:
             native = (exchange != "p2p" and self.device.type == "cuda" and
                       (world == 1 or self._nccl_group()))
         if native:
+            err = None
             try:
                 self._native = NativeShardedStep(plan, rank, world, batch, dtype, self.device,
                                                  group, exchange, self.chunks,
@@ -216,12 +217,20 @@ class ShardedMapLookup:
             except _lib.EmbtabError as e:
                 if not auto:
                     raise
-                # the auto choice falls back to the torch.distributed exchange (same
-                # plan, same kernels, same results) when the library's RCCL communicator
-                # cannot be made; an explicit native=True request raises instead
+                err = e
+            if auto and world > 1 and not self._all_ranks_ok(err is None):
+                # every rank takes the same exchange: if any rank could not make the
+                # library's communicator, all of them close theirs and use the
+                # torch.distributed exchange (same plan, same kernels, same results)
+                if self._native is not None:
+                    self._native.close()
+                    self._native = None
+                if err is None:
+                    err = _lib.EmbtabError("another rank could not make the RCCL communicator")
+            if err is not None:
                 import warnings
 
-                warnings.warn(f"native sharded step unavailable ({e}); using the "
+                warnings.warn(f"native sharded step unavailable ({err}); using the "
                               "torch.distributed exchange")
                 self._native = None
         if self._native is not None:
@@ -412,6 +421,15 @@ class ShardedMapLookup:
         return self.out
 
     # --- the exchange -------------------------------------------------------------------
+    def _all_ranks_ok(self, ok: bool) -> bool:
+        """MIN over the ranks of `ok` (a collective of the process group)."""
+        import torch.distributed as dist
+
+        dev = self.device if self._nccl_group() else torch.device("cpu")
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
+
     def _nccl_group(self) -> bool:
         import torch.distributed as dist
 
@@ -641,14 +659,26 @@ def make_comm(group, rank: int, world: int) -> ctypes.c_void_p:
     (on the current device).  World 1 needs no broadcast."""
     L = _lib.load()
     idbuf = (ctypes.c_char * _lib.ET_COMM_ID_BYTES)()
+    err = None
     if rank == 0:
-        _lib.check(L.et_comm_unique_id(ctypes.addressof(idbuf)))
+        try:
+            _lib.check(L.et_comm_unique_id(ctypes.addressof(idbuf)))
+        except _lib.EmbtabError as e:
+            if world == 1:
+                raise
+            err = e
     if world > 1:
         import torch.distributed as dist
 
-        obj = [bytes(idbuf) if rank == 0 else None]
+        # rank 0 always broadcasts (an empty id if it failed), so no rank is left
+        # waiting for an id that never comes
+        obj = [(b"" if err else bytes(idbuf)) if rank == 0 else None]
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast_object_list(obj, src=src, group=group)
+        if err is not None:
+            raise err
+        if not obj[0]:
+            raise _lib.EmbtabError("rank 0 could not make an RCCL unique id")
         idbuf = (ctypes.c_char * _lib.ET_COMM_ID_BYTES).from_buffer_copy(obj[0])
     comm = ctypes.c_void_p()
     _lib.check(L.et_comm_init(ctypes.byref(comm), world, ctypes.addressof(idbuf), rank))

@@ -162,3 +162,56 @@ def test_compact_piece_tables_hold_only_the_slice():
     assert c.data.untyped_storage().nbytes() == 40 * 64 * 4
     assert c.lookup_type == et.Static(64)
     assert compact_piece_table(full, Piece(3, 0, 128, 7)) is full
+
+
+def _comm_fail_worker(rank, world, port, result_q):
+    import embtab.sharding as sh
+    from embtab import _lib
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class FailingL:
+        """Library stand-in whose et_comm_unique_id fails (rank 0 only calls it)."""
+
+        def et_comm_unique_id(self, buf):
+            return 5
+
+        def et_last_error(self):
+            return b"no RCCL here"
+
+        def et_comm_init(self, *a):
+            raise AssertionError("et_comm_init reached after a failed unique id")
+
+    real = _lib.load
+    _lib.load = lambda: FailingL()
+    try:
+        sh.make_comm(None, rank, world)
+        raised = False
+    except _lib.EmbtabError:
+        raised = True
+    finally:
+        _lib.load = real
+    sm = sh.ShardedMapLookup.__new__(sh.ShardedMapLookup)
+    sm.device, sm.group = torch.device("cpu"), None
+    agree_fail = sm._all_ranks_ok(rank != 1)  # one rank failed -> every rank sees False
+    agree_ok = sm._all_ranks_ok(True)
+    result_q.put((rank, raised, agree_fail, agree_ok))
+    dist.destroy_process_group()
+
+
+def test_native_step_fallback_is_collective():
+    """A failed RCCL unique id on rank 0 raises on every rank (rank 0 broadcasts an empty
+    id instead of leaving the others blocked), and the auto fallback is decided by a MIN
+    over the ranks, so every rank takes the same exchange."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_fail_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert res == [(0, True, False, True), (1, True, False, True)], res
