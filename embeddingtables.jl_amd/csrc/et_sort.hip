@@ -20,6 +20,7 @@ namespace et {
 constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanThreads * kScanItems;  // 4096
+constexpr int kScanPartialsLds = 16384;               // partials staged in LDS (64 KB)
 
 constexpr int kRsMaxBits = 9;  // digit width: 9 bits -> 3 passes for keys < 2^27
 constexpr int kRsMaxBuckets = 1 << kRsMaxBits;
@@ -85,20 +86,47 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_partials(uint32_t* __rest
                                                                 const uint32_t* __restrict__ mlen,
                                                                 uint32_t madd) {
     __shared__ uint32_t lds4[4];
-    uint32_t carry = 0;
     if (mlen) {  // tiles past the device-side length hold zeros and are never read
         const int64_t used = ((int64_t)*mlen + madd + kScanTile - 1) / kScanTile;
         np = used < np ? used : np;
     }
-    for (int64_t b0 = 0; b0 < np; b0 += kScanThreads) {
-        const int64_t i = b0 + threadIdx.x;
-        const uint32_t v = i < np ? part[i] : 0u;
-        uint32_t total;
-        const uint32_t inc = block_inclusive_scan_256(v, lds4, &total);
-        if (i < np) part[i] = carry + inc - v;
-        carry += total;
+    // one block scan: thread t owns the contiguous run [t*per, (t+1)*per) (a loop of
+    // 256-wide block scans costs two barriers and a dependent load per 256 entries —
+    // 26 us for the 8.3 K tiles of a 34 M-key segment scan)
+    // Up to 16384 partials (a 64 M-element scan) are staged in LDS with coalesced loads
+    // and stores; the per-thread runs then read LDS instead of strided global words.
+    __shared__ uint32_t sp[kScanPartialsLds];
+    const bool staged = np <= kScanPartialsLds;  // workgroup-uniform
+    uint32_t* p = staged ? sp : part;
+    if (staged) {  // all loads issued before the LDS stores (one memory latency)
+        uint32_t buf[kScanPartialsLds / kScanThreads];
+#pragma unroll
+        for (int r = 0; r < kScanPartialsLds / kScanThreads; ++r) {
+            const int64_t i = r * kScanThreads + threadIdx.x;
+            buf[r] = i < np ? part[i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < kScanPartialsLds / kScanThreads; ++r)
+            sp[r * kScanThreads + threadIdx.x] = buf[r];
+        __syncthreads();
     }
-    if (threadIdx.x == 0) part[np] = carry;
+    const int64_t per = (np + kScanThreads - 1) / kScanThreads;
+    const int64_t i0 = (int64_t)threadIdx.x * per;
+    const int64_t i1 = i0 + per < np ? i0 + per : np;
+    uint32_t s = 0;
+    for (int64_t i = i0; i < i1; ++i) s += p[i];
+    uint32_t total;
+    uint32_t run = block_inclusive_scan_256(s, lds4, &total) - s;
+    for (int64_t i = i0; i < i1; ++i) {
+        const uint32_t v = p[i];
+        p[i] = run;
+        run += v;
+    }
+    if (staged) {
+        __syncthreads();
+        for (int64_t i = threadIdx.x; i < np; i += kScanThreads) part[i] = sp[i];
+    }
+    if (threadIdx.x == 0) part[np] = total;
 }
 
 // Blocked per-thread segments: thread t scans elements [t*16, t*16+16) of the tile.
@@ -205,6 +233,25 @@ __device__ __forceinline__ uint32_t rs_digit(uint32_t key, uint32_t base, uint32
     return (l >> shift) & (NB - 1);
 }
 
+// LDS digit-count increment of one wave instruction whose lanes hold consecutive
+// elements (valid lanes a prefix): equal digits in adjacent lanes are added once per run
+// by the run's first lane.  A skewed tile — a Zipf-hot column, or a table of a few rows,
+// whose keys are nearly all equal — otherwise serialises up to 64 lane atomics on one
+// LDS address (the last sort pass's histogram took 87 us for 34 M keys, the first pass's
+// 12 us for 7.9 M keys of the large tables).
+__device__ __forceinline__ void lds_count_runs(uint32_t* row, uint32_t d, bool valid) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t prev = (uint32_t)__shfl_up((int)d, 1, 64);
+    const bool head = valid && (lane == 0 || d != prev);
+    const uint64_t heads = (uint64_t)__ballot(head);
+    const int nvalid = __popcll((uint64_t)__ballot(valid));
+    if (head) {
+        const uint64_t after = lane < 63 ? heads >> (lane + 1) : 0ull;
+        const int end = after ? lane + __ffsll((long long)after) : nvalid;
+        atomicAdd(&row[d], (uint32_t)(end - lane));
+    }
+}
+
 template <int BITS>
 __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restrict__ keys,
                                                         RsPass p, uint32_t* __restrict__ hist) {
@@ -229,7 +276,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(const uint32_t* __restri
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const uint32_t i = base + (r0 + q) * kRsThreads + threadIdx.x;
-            if (i < n) atomicAdd(&h[wave][rs_digit<NB>(kk[q], kb, cap, sh)], 1u);
+            lds_count_runs(h[wave], rs_digit<NB>(kk[q], kb, cap, sh), i < n);
         }
     }
     __syncthreads();
@@ -315,7 +362,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
         const uint32_t* wk = skey + wave * kPer;
         const uint32_t* wv = sval + wave * kPer;
         for (int rr = 0; rr < kPer; rr += 64)
-            atomicAdd(&wcnt[wave][rs_digit<NB>(wk[rr + lane], kb, cap, sh)], 1u);
+            lds_count_runs(wcnt[wave], rs_digit<NB>(wk[rr + lane], kb, cap, sh), true);
         __syncthreads();
         {
             // exclusive scan of the tile's digit totals (NB / 256 digits per thread)

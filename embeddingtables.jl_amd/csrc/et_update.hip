@@ -56,7 +56,12 @@ __device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, ui
 struct KeyGrid {
     uint32_t blk_off[ET_MAX_TABLES_PER_LAUNCH + 1];
     uint32_t in_b;  // bit t: table t's pairs go to the second sort buffer (see et_sort.hip)
+    uint32_t vec;   // bit t: contiguous 16-B aligned indices and 16-B aligned pair slots
 };
+
+// 4 occurrences per thread: two 16-byte index loads, one 16-byte key and one 16-byte
+// value store (config 4: 273 MB of indices in, 273 MB of pairs out).
+typedef long long i64x2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg, int ntables,
                                                     uint32_t* __restrict__ ka,
@@ -75,8 +80,31 @@ __global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg,
     const uint64_t nr = (uint64_t)d.nrows;
     const uint32_t nblk = kg.blk_off[t + 1] - kg.blk_off[t];
     int bad = 0;
-    for (uint32_t ol = (blockIdx.x - kg.blk_off[t]) * 256u + threadIdx.x; ol < n_t;
-         ol += nblk * 256u) {
+    uint32_t ol0 = (blockIdx.x - kg.blk_off[t]) * 256u + threadIdx.x;
+    if ((kg.vec >> t) & 1u) {  // workgroup-uniform
+        const uint32_t n4 = n_t / 4u;
+        const i64x2* ip = reinterpret_cast<const i64x2*>(d.idx);
+        for (uint32_t q = ol0; q < n4; q += nblk * 256u) {
+            const i64x2 a = ip[2 * q], b = ip[2 * q + 1];
+            const uint64_t c[4] = {(uint64_t)(a.x - 1), (uint64_t)(a.y - 1), (uint64_t)(b.x - 1),
+                                   (uint64_t)(b.y - 1)};
+            u32x4 kv, vv;
+            uint32_t kk[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool ok = c[j] < nr;
+                bad += ok ? 0 : 1;
+                kk[j] = ok ? r0 + (uint32_t)c[j] : sent;
+            }
+            kv.x = kk[0], kv.y = kk[1], kv.z = kk[2], kv.w = kk[3];
+            const uint32_t o = o0 + 4u * q;
+            vv.x = o, vv.y = o + 1u, vv.z = o + 2u, vv.w = o + 3u;
+            *reinterpret_cast<u32x4*>(keys + o) = kv;
+            *reinterpret_cast<u32x4*>(vals + o) = vv;
+        }
+        ol0 = 4u * n4 + (blockIdx.x - kg.blk_off[t]) * 256u + threadIdx.x;  // the < 4 left
+    }
+    for (uint32_t ol = ol0; ol < n_t; ol += nblk * 256u) {
         const uint32_t j = ol / pool, i = ol - j * pool;
         const uint64_t col = (uint64_t)(d.idx[(int64_t)j * d.ld_idx + i] - 1);
         const bool ok = col < nr;
@@ -92,8 +120,23 @@ __global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg,
 // one), fused into a tile scan: k_seg_reduce counts heads per 4096-key tile,
 // k_scan_partials scans the tile counts, k_seg_down recomputes the flags of its tile,
 // scans them and writes seg_start[segment] = position (and U, seg_start[U] = n).
-__device__ __forceinline__ uint32_t seg_head(const uint32_t* __restrict__ keys, int64_t i) {
-    return (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+// Head flags of keys [i, i + 4) (i a multiple of 4): one 16-byte load of the four keys
+// and one load of the key before them (an L1 hit but at a tile's first lane), instead
+// of two 4-byte loads per key.
+__device__ __forceinline__ void seg_heads4(const uint32_t* __restrict__ keys, int64_t n,
+                                           int64_t i, uint32_t (&h)[4]) {
+    uint32_t k[4];
+    if (i + 3 < n) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(keys + i);
+        k[0] = v.x, k[1] = v.y, k[2] = v.z, k[3] = v.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = i + j < n ? keys[i + j] : 0u;
+    }
+    const uint32_t prev = i > 0 ? keys[i - 1] : ~k[0];
+    h[0] = (i < n && k[0] != prev) ? 1u : 0u;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) h[j] = (i + j < n && k[j] != k[j - 1]) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_seg_reduce(const uint32_t* __restrict__ keys,
@@ -103,9 +146,10 @@ __global__ __launch_bounds__(kScanThreads) void k_seg_reduce(const uint32_t* __r
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
     uint32_t h = 0;
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {
-        const int64_t i = base + r * kScanThreads + threadIdx.x;
-        if (i < n) h += seg_head(keys, i);
+    for (int r = 0; r < kScanItems / 4; ++r) {  // striped 16-byte groups, coalesced
+        uint32_t f[4];
+        seg_heads4(keys, n, base + 4 * (r * kScanThreads + threadIdx.x), f);
+        h += f[0] + f[1] + f[2] + f[3];
     }
     uint32_t total;
     block_inclusive_scan_256(h, lds4, &total);
@@ -121,10 +165,12 @@ __global__ __launch_bounds__(kScanThreads) void k_seg_down(const uint32_t* __res
     __shared__ uint32_t tile[kScanTile + kScanTile / 32];
     const int64_t base = (int64_t)blockIdx.x * kScanTile;
 #pragma unroll
-    for (int r = 0; r < kScanItems; ++r) {  // striped, coalesced
-        const int e = r * kScanThreads + threadIdx.x;
-        const int64_t i = base + e;
-        tile[e + (e >> 5)] = i < n ? seg_head(keys, i) : 0u;
+    for (int r = 0; r < kScanItems / 4; ++r) {  // striped 16-byte groups, coalesced
+        const int e = 4 * (r * kScanThreads + threadIdx.x);
+        uint32_t f[4];
+        seg_heads4(keys, n, base + e, f);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tile[e + j + ((e + j) >> 5)] = f[j];
     }
     __syncthreads();
     uint32_t v[kScanItems];
@@ -152,25 +198,53 @@ __global__ __launch_bounds__(kScanThreads) void k_seg_down(const uint32_t* __res
 
 // nchunks per segment (0 beyond U), multi-chunk partial slots per segment; multi-chunk
 // segments are also appended to `mlist` (order irrelevant: each is reduced by exactly
-// one workgroup in a fixed order, so results do not depend on it).
+// one workgroup in a fixed order, so results do not depend on it).  The appends are
+// aggregated per workgroup round of kSegChunkItems x 256 segments (a block scan of the
+// threads' counts, one atomic): the multi-chunk segments are spread over the whole
+// segment list (8.5 K of 1.9 M on the config-4 batch), so per-segment atomics on the
+// one counter were serialised — 45 us for the pass.
+constexpr int kSegChunkItems = 8;
+
 __global__ __launch_bounds__(256) void k_seg_chunks(const uint32_t* __restrict__ seg_start,
                                                     int64_t n, uint32_t* __restrict__ counters,
                                                     uint32_t chunk, uint32_t* __restrict__ nch,
                                                     uint32_t* __restrict__ multi,
                                                     uint32_t* __restrict__ mlist) {
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t base_lds;
     // grid-stride over entries 0..U only (U is known on the device; the scans below
-    // stop at U + 1), so a fixed grid covers any n
-    const uint32_t U = counters[kCntU];
-    for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u <= (int64_t)U && u <= n;
-         u += (int64_t)gridDim.x * 256) {
-        uint32_t c = 0;
-        if (u < U) {
-            const uint32_t len = seg_start[u + 1] - seg_start[u];
-            c = len <= chunk ? 1u : (len + chunk - 1) / chunk;
+    // stop at U + 1), so a fixed grid covers any n; the loop bound is workgroup-uniform
+    const int64_t U = (int64_t)counters[kCntU];
+    const int64_t last = U < n ? U : n;
+    constexpr int64_t kRound = (int64_t)kSegChunkItems * 256;
+    for (int64_t u0 = (int64_t)blockIdx.x * kRound; u0 <= last;
+         u0 += (int64_t)gridDim.x * kRound) {
+        uint32_t c[kSegChunkItems];
+        uint32_t mine = 0;
+#pragma unroll
+        for (int j = 0; j < kSegChunkItems; ++j) {
+            const int64_t u = u0 + j * 256 + threadIdx.x;  // coalesced
+            c[j] = 0;
+            if (u < U) {
+                const uint32_t len = seg_start[u + 1] - seg_start[u];
+                c[j] = len <= chunk ? 1u : (len + chunk - 1) / chunk;
+            }
+            if (u <= last) {
+                nch[u] = c[j];
+                multi[u] = c[j] > 1 ? c[j] : 0u;
+            }
+            mine += c[j] > 1 ? 1u : 0u;
         }
-        nch[u] = c;
-        multi[u] = c > 1 ? c : 0u;
-        if (c > 1) mlist[atomicAdd(&counters[kCntM], 1u)] = (uint32_t)u;
+        uint32_t total;
+        uint32_t at = block_inclusive_scan_256(mine, lds4, &total) - mine;
+        if (total == 0) continue;  // workgroup-uniform
+        if (threadIdx.x == 0) base_lds = atomicAdd(&counters[kCntM], total);
+        __syncthreads();
+        at += base_lds;
+#pragma unroll
+        for (int j = 0; j < kSegChunkItems; ++j)
+            if (c[j] > 1) mlist[at++] = (uint32_t)(u0 + j * 256 + threadIdx.x);
+        __syncthreads();  // base_lds is rewritten next round
     }
 }
 
@@ -484,10 +558,10 @@ struct SingleTab {
 };
 
 template <int D, int MODE, bool NT>
-__global__ __launch_bounds__(256) void k_sgd_singles(
-    UpdatePack pack, int ntables, const uint32_t* __restrict__ vals,
+__device__ __forceinline__ void sgd_singles_body(
+    const UpdatePack& pack, int ntables, const uint32_t* __restrict__ vals,
     const ChunkRec* __restrict__ recs, const uint32_t* __restrict__ counters, uint32_t sent,
-    float eta32, double eta64, uint32_t my_mask) {
+    float eta32, double eta64, uint32_t my_mask, uint32_t bid, uint32_t nblk) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -505,8 +579,8 @@ __global__ __launch_bounds__(256) void k_sgd_singles(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane / LPR, sub = lane % LPR;
     const uint32_t C = counters[kCntC];
-    const uint32_t nwaves = gridDim.x * 4u;
-    const uint32_t wid = blockIdx.x * 4u + wave;
+    const uint32_t nwaves = nblk * 4u;
+    const uint32_t wid = bid * 4u + wave;
     for (uint32_t it = 0; (uint64_t)it * 64u * nwaves + wid < C; ++it) {
         // one record per lane: singles get their table-column and Δ-column addresses
         const uint64_t cl = ((uint64_t)it * 64u + lane) * nwaves + wid;
@@ -590,12 +664,12 @@ __global__ __launch_bounds__(256) void k_sgd_singles(
 // G + NG, ... sequentially (U rows in flight), the NR sums are added in range order
 // through LDS and group 0 applies the update.  Fixed partition => deterministic.
 template <int D, int MODE, bool NT>
-__global__ __launch_bounds__(256) void k_sgd_combine(
-    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+__device__ __forceinline__ void sgd_combine_body(
+    const UpdatePack& pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
     const uint32_t* __restrict__ counters, const uint32_t* __restrict__ mlist,
     const float* __restrict__ partials, int pdim, uint32_t sent, float eta32, double eta64,
-    uint32_t my_mask) {
+    uint32_t my_mask, uint32_t bid, uint32_t nblk) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -608,7 +682,7 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
     const int G = threadIdx.x / LPR, sub = lane % LPR;
     const uint32_t M = counters[kCntM];
     {
-        for (uint32_t k = blockIdx.x; k < M; k += gridDim.x) {
+        for (uint32_t k = bid; k < M; k += nblk) {
             const uint32_t seg = mlist[k];
             if (seg == kRetired) continue;  // a hot column (k_hot_pick), uniform
             {
@@ -682,6 +756,50 @@ __global__ __launch_bounds__(256) void k_sgd_combine(
             __syncthreads();
         }
     }
+}
+
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_singles(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ vals,
+    const ChunkRec* __restrict__ recs, const uint32_t* __restrict__ counters, uint32_t sent,
+    float eta32, double eta64, uint32_t my_mask) {
+    sgd_singles_body<D, MODE, NT>(pack, ntables, vals, recs, counters, sent, eta32, eta64,
+                                  my_mask, blockIdx.x, gridDim.x);
+}
+
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_combine(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
+    const uint32_t* __restrict__ counters, const uint32_t* __restrict__ mlist,
+    const float* __restrict__ partials, int pdim, uint32_t sent, float eta32, double eta64,
+    uint32_t my_mask) {
+    sgd_combine_body<D, MODE, NT>(pack, ntables, keys, seg_start, partial_start, counters, mlist,
+                                  partials, pdim, sent, eta32, eta64, my_mask, blockIdx.x,
+                                  gridDim.x);
+}
+
+// The combine and the singles in one launch: the first `ncomb` workgroups combine, the
+// rest update single-occurrence columns.  They touch disjoint columns (multi-chunk vs
+// single-occurrence segments) and both only follow the chunk pass, so the combine's
+// long sequential range sums (the hottest column's 3.3 K partials: 8 ranges of ~400
+// dependent row loads, ~80 us on its own) run under the singles' bandwidth-bound work
+// instead of after it.  Every workgroup takes one branch (block-uniform).
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_tail(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
+    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ partial_start,
+    const uint32_t* __restrict__ counters, const uint32_t* __restrict__ mlist,
+    const float* __restrict__ partials, int pdim, uint32_t sent, float eta32, double eta64,
+    uint32_t my_mask, uint32_t ncomb) {
+    if (blockIdx.x < ncomb)
+        sgd_combine_body<D, MODE, NT>(pack, ntables, keys, seg_start, partial_start, counters,
+                                      mlist, partials, pdim, sent, eta32, eta64, my_mask,
+                                      blockIdx.x, ncomb);
+    else
+        sgd_singles_body<D, MODE, NT>(pack, ntables, vals, recs, counters, sent, eta32, eta64,
+                                      my_mask, blockIdx.x - ncomb, gridDim.x - ncomb);
 }
 
 // Hot-column pass (non-exact Float32 mode, dim 128, pool <= 32).  The columns with the
@@ -1096,9 +1214,16 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
     KeyGrid kg;
     kg.blk_off[0] = 0;
+    kg.vec = 0;
+    const bool bufs16 = (((uintptr_t)w.ka | (uintptr_t)w.va | (uintptr_t)w.kb | (uintptr_t)w.vb) &
+                         15u) == 0;
     for (int t = 0; t < ntables; ++t) {
         const int64_t nt = pack.occ_off[t + 1] - pack.occ_off[t];
-        int64_t nb = cdiv64(nt, 256);
+        const et_update_desc& d = pack.d[t];
+        const bool vec = bufs16 && (d.ld_idx == d.pool || d.batch == 1) &&
+                         ((uintptr_t)d.idx & 15u) == 0 && (pack.occ_off[t] & 3u) == 0;
+        if (vec) kg.vec |= 1u << t;
+        int64_t nb = cdiv64(nt, vec ? 1024 : 256);
         nb = nb < 2048 ? nb : 2048;  // grid-stride beyond 2048 workgroups per table
         kg.blk_off[t + 1] = kg.blk_off[t] + (uint32_t)nb;
     }
@@ -1127,7 +1252,9 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     }
     const int64_t blocks1 = cdiv64(n + 1, 256);
     const unsigned fixed_grid = (unsigned)(blocks1 < 8192 ? blocks1 : 8192);
-    hipLaunchKernelGGL(k_seg_chunks, dim3(fixed_grid), dim3(256), 0, s, w.seg_start, n,
+    const int64_t sc_blocks = cdiv64(n + 1, (int64_t)kSegChunkItems * 256);
+    hipLaunchKernelGGL(k_seg_chunks, dim3((unsigned)(sc_blocks < 2048 ? sc_blocks : 2048)),
+                       dim3(256), 0, s, w.seg_start, n,
                        w.counters, chunk, w.nch, w.multi, w.mlist);
     ET_LAUNCH_CHECK("k_seg_chunks");
     // nch -> chunk_start, multi -> partial_start (in place, n+1 entries)
@@ -1193,6 +1320,7 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                      const HotList& hl, unsigned grid) {
     if constexpr (__is_same(T, float)) {
         const bool singles = sgd_singles();
+        const unsigned ncomb = grid < 2048u ? grid : 2048u;  // combine workgroups of k_sgd_tail
         if (hl.n > 0 && w.hot_part) {
             hipLaunchKernelGGL(k_sgd_hot, dim3((unsigned)w.hot_nw, (unsigned)hl.n), dim3(256), 0, s,
                                pack, hl, w.hot_cnt, w.hot_slots, w.hot_part, w.hot_nw);
@@ -1208,12 +1336,14 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                            ntables, gr.keys, gr.vals, w.recs, w.counters, w.partials, pdim,    \
                            sent, eta_c, eta64, vg.mask[i], singles ? 1 : 0);                   \
         if (singles)                                                                           \
-            hipLaunchKernelGGL((k_sgd_singles<DD, MODE, NT>), dim3(grid), dim3(256), 0, s,     \
-                               pack, ntables, gr.vals, w.recs, w.counters, sent, eta_c, eta64, \
-                               vg.mask[i]);                                                    \
-        hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,   \
-                           ntables, gr.keys, w.seg_start, w.multi, w.counters, w.mlist,        \
-                           w.partials, pdim, sent, eta_c, eta64, vg.mask[i]);                  \
+            hipLaunchKernelGGL((k_sgd_tail<DD, MODE, NT>), dim3(grid + ncomb), dim3(256), 0, s, \
+                               pack, ntables, gr.keys, gr.vals, w.recs, w.seg_start, w.multi,  \
+                               w.counters, w.mlist, w.partials, pdim, sent, eta_c, eta64,      \
+                               vg.mask[i], ncomb);                                             \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_sgd_combine<DD, MODE, NT>), dim3(grid), dim3(256), 0, s,     \
+                               pack, ntables, gr.keys, w.seg_start, w.multi, w.counters,       \
+                               w.mlist, w.partials, pdim, sent, eta_c, eta64, vg.mask[i]);     \
         break;
         for (int i = 0; i < vg.n; ++i) switch (vg.cap[i]) {
             ET_SGD_VEC(16)
