@@ -238,7 +238,9 @@ __device__ __forceinline__ uint32_t rs_digit(uint32_t key, uint32_t base, uint32
 // by the run's first lane.  A skewed tile — a Zipf-hot column, or a table of a few rows,
 // whose keys are nearly all equal — otherwise serialises up to 64 lane atomics on one
 // LDS address (the last sort pass's histogram took 87 us for 34 M keys, the first pass's
-// 12 us for 7.9 M keys of the large tables).
+// 12 us for 7.9 M keys of the large tables).  Not used in the staged scatter's counts:
+// there the extra ballots cost more than the conflicts (passes over the large tables
+// 51 / 140 us -> 56 / 160 us, the last pass unchanged).
 __device__ __forceinline__ void lds_count_runs(uint32_t* row, uint32_t d, bool valid) {
     const int lane = threadIdx.x & 63;
     const uint32_t prev = (uint32_t)__shfl_up((int)d, 1, 64);
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_scatter(
         const uint32_t* wk = skey + wave * kPer;
         const uint32_t* wv = sval + wave * kPer;
         for (int rr = 0; rr < kPer; rr += 64)
-            lds_count_runs(wcnt[wave], rs_digit<NB>(wk[rr + lane], kb, cap, sh), true);
+            atomicAdd(&wcnt[wave][rs_digit<NB>(wk[rr + lane], kb, cap, sh)], 1u);
         __syncthreads();
         {
             // exclusive scan of the tile's digit totals (NB / 256 digits per thread)

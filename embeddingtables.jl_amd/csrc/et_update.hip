@@ -663,6 +663,8 @@ __device__ __forceinline__ void sgd_singles_body(
 // a shard's piece — combines exactly like the whole table); lane group G sums ranges G,
 // G + NG, ... sequentially (U rows in flight), the NR sums are added in range order
 // through LDS and group 0 applies the update.  Fixed partition => deterministic.
+constexpr uint32_t kLongPartials = 64;
+
 template <int D, int MODE, bool NT>
 __device__ __forceinline__ void sgd_combine_body(
     const UpdatePack& pack, int ntables, const uint32_t* __restrict__ keys,
@@ -681,10 +683,16 @@ __device__ __forceinline__ void sgd_combine_body(
     const int lane = threadIdx.x & 63;
     const int G = threadIdx.x / LPR, sub = lane % LPR;
     const uint32_t M = counters[kCntM];
-    {
+    // two sweeps over the list: segments of more than kLongPartials partials first, so
+    // the long sequential range sums (latency chains) start with the kernel, the rest after
+    for (int sweep = 0; sweep < 2; ++sweep) {
         for (uint32_t k = bid; k < M; k += nblk) {
             const uint32_t seg = mlist[k];
             if (seg == kRetired) continue;  // a hot column (k_hot_pick), uniform
+            {
+                const uint32_t npp = partial_start[seg + 1] - partial_start[seg];
+                if ((npp > kLongPartials) != (sweep == 0)) continue;  // uniform
+            }
             {
                 const uint32_t key0 = keys[seg_start[seg]];
                 if (key0 == sent || !((my_mask >> table_of_key(pack, ntables, key0)) & 1u))
@@ -1320,7 +1328,9 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                      const HotList& hl, unsigned grid) {
     if constexpr (__is_same(T, float)) {
         const bool singles = sgd_singles();
-        const unsigned ncomb = grid < 2048u ? grid : 2048u;  // combine workgroups of k_sgd_tail
+        // combine workgroups of k_sgd_tail: a quarter of one resident wave of workgroups,
+        // so the singles start at once beside them
+        const unsigned ncomb = grid < 256u ? grid : 256u;
         if (hl.n > 0 && w.hot_part) {
             hipLaunchKernelGGL(k_sgd_hot, dim3((unsigned)w.hot_nw, (unsigned)hl.n), dim3(256), 0, s,
                                pack, hl, w.hot_cnt, w.hot_slots, w.hot_part, w.hot_nw);
