@@ -642,3 +642,76 @@ def test_phased_hot_pass_null_delta_index_phase():
     torch.cuda.synchronize()
     assert torch.equal(one, two)
     assert not torch.equal(one, dev(base))
+
+
+def test_update_index_layouts_and_skew(oracle):
+    """The key build's 16-byte path and its fallbacks, and skewed sort tiles: index
+    buffers that are contiguous with a tail (n % 4 != 0), a strided view (ld_idx >
+    pool), 8-byte aligned (storage offset 1), tables whose occurrence offset in a
+    multi-table call is not a multiple of 4, and a 3-row table hit 90% by one column
+    (one LDS address per run in the radix histogram).  Exact mode: bit-identical to
+    the oracle; default mode on the same inputs: bit-identical wherever a column has
+    at most ET_SGD_CHUNK occurrences."""
+    from embtab.tables import fused_update_path
+
+    rng = np.random.default_rng(77)
+
+    def contiguous(B, P, R):
+        return dev(rng.integers(1, R + 1, (B, P)))
+
+    def strided(B, P, R):
+        big = dev(rng.integers(1, R + 1, (B, P + 5)))
+        return big[:, 2:2 + P]
+
+    def offset1(B, P, R):
+        buf = torch.empty(B * P + 1, dtype=torch.int64, device=DEV)
+        v = buf[1:].view(B, P)
+        v.copy_(dev(rng.integers(1, R + 1, (B, P))))
+        assert v.data_ptr() % 16 == 8
+        return v
+
+    def skewed(B, P, R):
+        I = np.where(rng.random((B, P)) < 0.9, 2, rng.integers(1, R + 1, (B, P)))
+        return dev(I)
+
+    cases = [(contiguous, 5, 3, 50), (strided, 7, 3, 40), (offset1, 33, 4, 60),
+             (skewed, 1000, 20, 3), (contiguous, 129, 1, 500)]
+    for exact in (True, False):
+        # one table at a time
+        for make, B, P, R in cases:
+            base = rng.standard_normal((R, 128)).astype(np.float32)
+            I = make(B, P, R)
+            delta = rng.standard_normal((B, 128)).astype(np.float32)
+            A = et.SimpleEmbedding(dev(base), et.Static(128))
+            g = et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), I)
+            et.update_(et.Descent(0.5), A, g, exact=exact)
+            ref = base.copy()
+            Ih = host(I)
+            oracle.sgd(ref, delta, Ih, 0.5, fused=fused_update_path(A))
+            counts = np.bincount(Ih.reshape(-1), minlength=R + 1)[1:]
+            ok = counts <= CHUNK if not exact else np.ones(R, bool)
+            got = host(A.data)
+            assert bits_equal(got[ok], ref[ok]), (make.__name__, B, P, R, exact)
+            if not ok.all():  # chunked columns: both within 1e-6 of |w| + eta * sum|delta|
+                absacc = np.zeros((R, 128))
+                np.add.at(absacc, Ih.reshape(-1) - 1, np.repeat(np.abs(delta), P, axis=0))
+                scale = np.abs(base) + 0.5 * absacc
+                assert np.all(np.abs(got[~ok] - ref[~ok]) <= 2e-6 * scale[~ok])
+        # all of them in one multi-table call (occurrence offsets 15, 36, 168, 20168)
+        tabs, grads, refs, hs = [], [], [], []
+        for make, B, P, R in [(c[0], 129, c[2], c[3]) for c in cases]:
+            base = rng.standard_normal((R, 128)).astype(np.float32)
+            I = make(B, P, R)
+            delta = rng.standard_normal((B, 128)).astype(np.float32)
+            A = et.SimpleEmbedding(dev(base), et.Static(128))
+            tabs.append(A)
+            grads.append(et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), I))
+            refs.append(base.copy())
+            hs.append((host(I), delta))
+        et.update_(et.Descent(0.5), tabs, grads, [et.Indexer() for _ in tabs], exact=exact)
+        for A, ref, (Ih, delta) in zip(tabs, refs, hs):
+            oracle.sgd(ref, delta, Ih, 0.5, fused=fused_update_path(A))
+            counts = np.bincount(Ih.reshape(-1), minlength=ref.shape[0] + 1)[1:]
+            ok = counts <= CHUNK if not exact else np.ones(ref.shape[0], bool)
+            assert bits_equal(host(A.data)[ok], ref[ok])
+    assert et.check_errors() == 0
