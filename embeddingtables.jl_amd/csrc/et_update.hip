@@ -464,8 +464,8 @@ __device__ __forceinline__ void apply_row(float* __restrict__ w,
 // the gradient sum (so the read overlaps the delta gathers) and apply the update;
 // chunks of longer segments store a partial row.
 template <int D, int MODE, bool NT>
-__global__ __launch_bounds__(256) void k_sgd_chunks(
-    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+__device__ __forceinline__ void sgd_chunks_body(
+    const UpdatePack& pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, float* __restrict__ partials, int pdim,
     uint32_t sent, float eta32, double eta64, uint32_t my_mask, int skip_singles) {
@@ -539,6 +539,25 @@ __global__ __launch_bounds__(256) void k_sgd_chunks(
         }
     }
 }
+
+#define ET_SGD_CHUNKS_ARGS                                                                     \
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,                           \
+        const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,                  \
+        const uint32_t* __restrict__ counters, float* __restrict__ partials, int pdim,         \
+        uint32_t sent, float eta32, double eta64, uint32_t my_mask, int skip_singles
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_chunks(ET_SGD_CHUNKS_ARGS) {
+    sgd_chunks_body<D, MODE, NT>(pack, ntables, keys, vals, recs, counters, partials, pdim, sent,
+                                 eta32, eta64, my_mask, skip_singles);
+}
+// The same pass compiled for 5 waves per SIMD (96 VGPRs instead of 97-104: 4 waves).
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chunks5(
+    ET_SGD_CHUNKS_ARGS) {
+    sgd_chunks_body<D, MODE, NT>(pack, ntables, keys, vals, recs, counters, partials, pdim, sent,
+                                 eta32, eta64, my_mask, skip_singles);
+}
+#undef ET_SGD_CHUNKS_ARGS
 
 // Single-occurrence columns (70% of the chunks on the config-4 batch, 1.34 M of 2.0 M):
 // in k_sgd_chunks each is a chain of dependent loads (record -> occurrence id -> Δ
@@ -1321,6 +1340,15 @@ inline bool sgd_singles() {
     return v;
 }
 
+// k_sgd_chunks5 (5 waves per SIMD) instead of k_sgd_chunks (ET_SGD_OCC5=0/1, for A/B).
+inline bool sgd_chunks_occ5() {
+    static const bool v = [] {
+        const char* e = getenv("ET_SGD_OCC5");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
@@ -1342,9 +1370,16 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         }
 #define ET_SGD_VEC(DD)                                                                         \
     case DD:                                                                                   \
-        hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,    \
-                           ntables, gr.keys, gr.vals, w.recs, w.counters, w.partials, pdim,    \
-                           sent, eta_c, eta64, vg.mask[i], singles ? 1 : 0);                   \
+        if (sgd_chunks_occ5())                                                                 \
+            hipLaunchKernelGGL((k_sgd_chunks5<DD, MODE, NT>), dim3(grid), dim3(256), 0, s,     \
+                               pack, ntables, gr.keys, gr.vals, w.recs, w.counters,            \
+                               w.partials, pdim, sent, eta_c, eta64, vg.mask[i],               \
+                               singles ? 1 : 0);                                               \
+        else                                                                                   \
+            hipLaunchKernelGGL((k_sgd_chunks<DD, MODE, NT>), dim3(grid), dim3(256), 0, s,      \
+                               pack, ntables, gr.keys, gr.vals, w.recs, w.counters,            \
+                               w.partials, pdim, sent, eta_c, eta64, vg.mask[i],               \
+                               singles ? 1 : 0);                                               \
         if (singles)                                                                           \
             hipLaunchKernelGGL((k_sgd_tail<DD, MODE, NT>), dim3(grid + ncomb), dim3(256), 0, s, \
                                pack, ntables, gr.keys, gr.vals, w.recs, w.seg_start, w.multi,  \
