@@ -1166,7 +1166,10 @@ inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
 inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
                                 int nhot = 0, int64_t hot_batch = 0, int64_t hot_bytes = 0) {
     UpdateWs w;
-    int64_t off = 0;
+    // every buffer 256-byte aligned whatever the caller's workspace alignment (the
+    // 16-byte key / index / LDS-DMA loads rely on it): the layout starts at the first
+    // 256-byte boundary of the workspace, and the size asks for 256 bytes of slack
+    int64_t off = base ? (int64_t)((256u - ((uintptr_t)base & 255u)) & 255u) : 256;
     auto take = [&](int64_t bytes) -> char* {
         char* p = base ? base + off : nullptr;
         off += align256(bytes);

@@ -183,7 +183,9 @@ typedef struct et_update_desc {
     int64_t cols_per_page; /* 0 or a paged table, as in et_lookup_desc */
 } et_update_desc;
 
-/* Bytes of device workspace needed by et_sparse_sgd for these descriptors. */
+/* Bytes of device workspace needed by et_sparse_sgd for these descriptors (any
+ * alignment: the library lays its buffers out from the workspace's first 256-byte
+ * boundary; the size includes that slack). */
 int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntables, int64_t* bytes);
 
 /* Fused sparse SGD (Flux.Descent) over one or many tables:

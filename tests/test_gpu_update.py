@@ -715,3 +715,36 @@ def test_update_index_layouts_and_skew(oracle):
             ok = counts <= CHUNK if not exact else np.ones(ref.shape[0], bool)
             assert bits_equal(host(A.data)[ok], ref[ok])
     assert et.check_errors() == 0
+
+
+@pytest.mark.parametrize("shift", [0, 4, 100])
+def test_update_workspace_at_any_alignment(shift):
+    """et_sparse_sgd lays its buffers out from the first 256-byte boundary of the
+    caller's workspace (et_sgd_workspace_size includes the slack), so a workspace at a
+    4-byte or 100-byte offset gives the same update as an aligned one."""
+    import ctypes
+
+    from embtab import _lib
+
+    L = _lib.load()
+    rng = np.random.default_rng(5)
+    B, P, D, R = 2000, 20, 128, 700
+    base = rng.standard_normal((R, D)).astype(np.float32)
+    I = np.minimum(rng.zipf(1.2, (B, P)), R)
+    delta = rng.standard_normal((B, D)).astype(np.float32)
+    dI, dd = dev(I), dev(delta)
+    outs = []
+    for sh in (0, shift):
+        tab = dev(base)
+        arr = (_lib.UpdateDesc * 1)(_lib.UpdateDesc(tab.data_ptr(), D, R, D, P, dd.data_ptr(), D,
+                                                    dI.data_ptr(), P, B, 0))
+        nb = ctypes.c_int64()
+        _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), 1, ctypes.byref(nb)))
+        ws = torch.empty(nb.value + sh, dtype=torch.uint8, device=DEV)
+        _lib.check(L.et_sparse_sgd(_lib.ET_F32, ctypes.addressof(arr), 1, 0.1,
+                                   _lib.ET_FLAG_NONTEMPORAL, ws.data_ptr() + sh, nb.value,
+                                   _lib.stream_handle()))
+        torch.cuda.synchronize()
+        outs.append(tab)
+    assert torch.equal(outs[0], outs[1])
+    assert not torch.equal(outs[0], dev(base))
