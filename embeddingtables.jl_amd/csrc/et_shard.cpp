@@ -13,8 +13,11 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <map>
+#include <mutex>
 #include <new>
 #include <set>
 #include <vector>
@@ -29,6 +32,152 @@ namespace et {
         if (r_ != ncclSuccess)                                                          \
             return ::et::fail(ET_ERR_HIP, "%s failed: %s", #call, ncclGetErrorString(r_)); \
     } while (0)
+
+// ---------------------------------------------------------------------------------------
+// Loopback communicator: N simulated ranks of ONE process (one host thread per rank, all
+// on the current GPU).  It lets the world > 1 code of the sharded step — gathered-chunk
+// offsets, all-to-all splits, the side-stream event pipeline — run unchanged without N
+// GPUs: every collective is a host rendezvous of the N callers, after which each rank
+// enqueues device copies from its peers' posted buffers on its own stream, ordered after
+// the peers' producers by events, and its stream is ordered after every copy that reads
+// its own send buffers (RCCL's completion semantics: a collective is done on a rank's
+// stream once its send buffers may be reused).
+// ---------------------------------------------------------------------------------------
+struct LoopPost {                 // what one rank posts for one collective
+    std::vector<const char*> send;  // per peer: the bytes this rank sends to it
+    std::vector<size_t> sbytes;
+    std::vector<char*> recv;        // per peer: where this rank receives from it
+    std::vector<size_t> rbytes;
+};
+
+struct LoopGroup {
+    int n = 0, live = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<LoopPost> post;
+    std::vector<hipEvent_t> ready, done;  // per rank: its sends produced / its copies done
+    int err = 0;                          // first failure of the current collective
+
+    bool broken = false;                  // a rank gave up waiting: the group is unusable
+
+    // generation barrier over the n ranks (host threads); false if a rank has not arrived
+    // within 120 s (a rank that failed before the collective never will)
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (broken) return false;
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) ||
+            broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+};
+
+struct LoopComm {
+    LoopGroup* g;
+    int rank;
+};
+
+static std::mutex g_loop_mu;
+static std::set<const void*> g_loop_comms;  // handles made by et_comm_loopback
+
+static LoopComm* as_loop(const void* comm) {
+    std::lock_guard<std::mutex> lk(g_loop_mu);
+    return g_loop_comms.count(comm) ? (LoopComm*)comm : nullptr;
+}
+
+// One loopback exchange: rank r sends send[p] (sbytes[p]) to every peer p and receives
+// recv[p] (rbytes[p]) from it.  Collective over the group's ranks; stream-ordered on st.
+static int loop_exchange(LoopComm* c, LoopPost&& mine, hipStream_t st) {
+    LoopGroup& g = *c->g;
+    const int r = c->rank;
+    hipError_t e = hipEventRecord(g.ready[r], st);
+    g.post[r] = std::move(mine);
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.err = ET_ERR_HIP;
+    }
+    if (!g.barrier())  // every rank's buffers and events are posted
+        return fail(ET_ERR_ARG, "loopback exchange: a rank did not join the collective");
+    int bad = 0;
+    {
+        std::lock_guard<std::mutex> lk(g.mu);
+        bad = g.err;
+        for (int p = 0; p < g.n && !bad; ++p)
+            if (g.post[p].sbytes.size() != (size_t)g.n || g.post[r].rbytes[p] != g.post[p].sbytes[r])
+                bad = ET_ERR_ARG;
+    }
+    for (int p = 0; p < g.n && !bad && e == hipSuccess; ++p) {
+        const size_t nb = g.post[r].rbytes[p];
+        if (!nb) continue;
+        if (p != r) e = hipStreamWaitEvent(st, g.ready[p], 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(g.post[r].recv[p], g.post[p].send[r], nb, hipMemcpyDeviceToDevice, st);
+    }
+    if (e == hipSuccess) e = hipEventRecord(g.done[r], st);
+    if (e != hipSuccess && !bad) {
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.err = ET_ERR_HIP;
+    }
+    if (!g.barrier())  // every rank's copies are enqueued
+        return fail(ET_ERR_ARG, "loopback exchange: a rank did not join the collective");
+    for (int p = 0; p < g.n && !bad && e == hipSuccess; ++p)
+        if (p != r) e = hipStreamWaitEvent(st, g.done[p], 0);
+    {
+        std::lock_guard<std::mutex> lk(g.mu);
+        if (e != hipSuccess && !g.err) g.err = ET_ERR_HIP;
+        bad = bad ? bad : g.err;
+    }
+    // everyone has read err; then the next collective starts clean
+    if (!g.barrier()) return fail(ET_ERR_ARG, "loopback exchange: a rank did not join the collective");
+    if (r == 0) {
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.err = 0;
+    }
+    if (!g.barrier()) return fail(ET_ERR_ARG, "loopback exchange: a rank did not join the collective");
+    if (bad == ET_ERR_ARG) return fail(ET_ERR_ARG, "loopback exchange: the ranks' send and receive sizes differ");
+    if (bad) return fail(ET_ERR_HIP, "loopback exchange: a HIP call failed on some rank");
+    return ET_OK;
+}
+
+static LoopPost loop_allgather_post(int n, int rank, const void* send, void* recv, size_t bytes) {
+    LoopPost m;
+    m.send.assign(n, (const char*)send);
+    m.sbytes.assign(n, bytes);
+    m.recv.resize(n);
+    m.rbytes.assign(n, bytes);
+    for (int p = 0; p < n; ++p) m.recv[p] = (char*)recv + size_t(p) * bytes;
+    (void)rank;
+    return m;
+}
+
+// Grouped point-to-point exchange over RCCL: rank sends send[p] to p and receives recv[p]
+// from p.  A failure inside the group still closes it (a group left open breaks every
+// later RCCL call of the thread).
+static int nccl_exchange(ncclComm_t comm, const LoopPost& m, hipStream_t st) {
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return fail(ET_ERR_HIP, "ncclGroupStart failed: %s", ncclGetErrorString(r));
+    const int n = (int)m.send.size();
+    for (int p = 0; p < n && r == ncclSuccess; ++p) {
+        if (m.sbytes[p]) r = ncclSend(m.send[p], m.sbytes[p], ncclUint8, p, comm, st);
+        if (r == ncclSuccess && m.rbytes[p]) r = ncclRecv(m.recv[p], m.rbytes[p], ncclUint8, p, comm, st);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(ET_ERR_HIP, "ncclSend/ncclRecv failed: %s", ncclGetErrorString(r));
+    if (r2 != ncclSuccess) return fail(ET_ERR_HIP, "ncclGroupEnd failed: %s", ncclGetErrorString(r2));
+    return ET_OK;
+}
 
 static const int kPieceDims[] = {512, 256, 128, 64, 32, 16};  // vector-kernel feature widths
 
@@ -123,7 +272,8 @@ struct Launch {  // one et_concat_slabs / et_split_slabs launch of the assembly
 };
 
 struct Sharded {
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;    // RCCL, or
+    LoopComm* loop = nullptr;     // a loopback rank (et_comm_loopback)
     int world = 0, rank = 0, dtype = 0, es = 0, chunks = 1, exchange = 0, device = 0;
     int64_t prepend = 0, ld_dst = 0, batch = 0, slab_ld = 0;
     std::vector<std::vector<et_shard_piece>> pieces;  // per rank, slab order
@@ -178,10 +328,14 @@ static ncclDataType_t bytes_type() { return ncclUint8; }
 static int exchange_chunk(Sharded& s, const char* slab_c, char* gath_c, int64_t nb, char* dst_c,
                           int64_t ld_dst, hipStream_t st) {
     const size_t bytes = size_t(nb) * s.slab_ld * s.es;
-    if (!s.comm)
+    if (s.loop) {
+        int rc = loop_exchange(s.loop, loop_allgather_post(s.world, s.rank, slab_c, gath_c, bytes), st);
+        if (rc != ET_OK) return rc;
+    } else if (!s.comm) {
         ET_HIP_CHECK(hipMemcpyAsync(gath_c, slab_c, bytes, hipMemcpyDeviceToDevice, st));
-    else
+    } else {
         ET_NCCL_CHECK(ncclAllGather(slab_c, gath_c, bytes, bytes_type(), s.comm, st));
+    }
     for (auto& L : s.launches) {
         int rc = et_concat_slabs(s.dtype, gath_c + L.shift * s.es, s.world, s.slab_ld, nb,
                                  L.rows.data(), L.offs.data(), dst_c, ld_dst, st);
@@ -269,9 +423,57 @@ extern "C" int et_comm_init(void** comm, int32_t nranks, const void* id, int32_t
     return ET_OK;
 }
 
+extern "C" int et_comm_loopback(void** comms, int32_t nranks) {
+    et::clear_err();
+    if (!comms || nranks <= 0 || nranks > 1024)
+        return et::fail(ET_ERR_ARG, "bad loopback arguments (nranks %d)", nranks);
+    et::LoopGroup* g = new (std::nothrow) et::LoopGroup();
+    if (!g) return et::fail(ET_ERR_ARG, "out of host memory");
+    g->n = g->live = nranks;
+    g->post.resize(nranks);
+    g->ready.assign(nranks, nullptr);
+    g->done.assign(nranks, nullptr);
+    hipError_t e = hipSuccess;
+    for (int r = 0; r < nranks && e == hipSuccess; ++r) {
+        e = hipEventCreateWithFlags(&g->ready[r], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        for (int r = 0; r < nranks; ++r) {
+            if (g->ready[r]) (void)hipEventDestroy(g->ready[r]);
+            if (g->done[r]) (void)hipEventDestroy(g->done[r]);
+        }
+        delete g;
+        return et::fail(ET_ERR_HIP, "event creation failed: %s", hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> lk(et::g_loop_mu);
+    for (int r = 0; r < nranks; ++r) {
+        comms[r] = new et::LoopComm{g, r};
+        et::g_loop_comms.insert(comms[r]);
+    }
+    return ET_OK;
+}
+
 extern "C" int et_comm_destroy(void* comm) {
     et::clear_err();
-    if (comm) ET_NCCL_CHECK(ncclCommDestroy((ncclComm_t)comm));
+    if (!comm) return ET_OK;
+    {
+        std::lock_guard<std::mutex> lk(et::g_loop_mu);
+        if (et::g_loop_comms.erase(comm)) {
+            et::LoopComm* c = (et::LoopComm*)comm;
+            et::LoopGroup* g = c->g;
+            delete c;
+            if (--g->live == 0) {  // the last rank of the group frees it
+                for (int r = 0; r < g->n; ++r) {
+                    (void)hipEventDestroy(g->ready[r]);
+                    (void)hipEventDestroy(g->done[r]);
+                }
+                delete g;
+            }
+            return ET_OK;
+        }
+    }
+    ET_NCCL_CHECK(ncclCommDestroy((ncclComm_t)comm));
     return ET_OK;
 }
 
@@ -288,10 +490,15 @@ extern "C" int et_allgather_concat(void* comm, int dtype, const void* slab, int6
     if (batch == 0) return ET_OK;
     hipStream_t st = (hipStream_t)stream;
     const size_t bytes = size_t(batch) * slab_ld * es;
-    if (!comm)
+    if (et::LoopComm* lc = et::as_loop(comm)) {
+        if (lc->g->n != nranks) return et::fail(ET_ERR_ARG, "loopback group of %d ranks, nranks %d", lc->g->n, nranks);
+        int rc = et::loop_exchange(lc, et::loop_allgather_post(nranks, lc->rank, slab, gathered, bytes), st);
+        if (rc != ET_OK) return rc;
+    } else if (!comm) {
         ET_HIP_CHECK(hipMemcpyAsync(gathered, slab, bytes, hipMemcpyDeviceToDevice, st));
-    else
+    } else {
         ET_NCCL_CHECK(ncclAllGather(slab, gathered, bytes, ncclUint8, (ncclComm_t)comm, st));
+    }
     return et_concat_slabs(dtype, gathered, nranks, slab_ld, batch, rows, dst_row_off, dst, ld_dst,
                            stream);
 }
@@ -314,7 +521,13 @@ extern "C" int et_sharded_create(void** handle, void* comm, int32_t world, int32
         return et::fail(ET_ERR_ARG, "bad batch / piece list");
     Sharded* s = new (std::nothrow) Sharded();
     if (!s) return et::fail(ET_ERR_ARG, "out of host memory");
-    s->comm = (ncclComm_t)comm;
+    s->loop = et::as_loop(comm);
+    s->comm = s->loop ? nullptr : (ncclComm_t)comm;
+    if (s->loop && (s->loop->g->n != world || s->loop->rank != rank)) {
+        delete s;
+        return et::fail(ET_ERR_ARG, "loopback communicator is rank %d of %d, not %d of %d",
+                        ((et::LoopComm*)comm)->rank, ((et::LoopComm*)comm)->g->n, rank, world);
+    }
     s->world = world;
     s->rank = rank;
     s->dtype = dtype;
@@ -413,16 +626,21 @@ extern "C" int et_sharded_maplookup(void* handle, const et_lookup_desc* local, i
         // DLRM layout: rank j keeps batch rows [split[j], split[j+1]) of every rank's slab
         if ((rc = et::lookup_chunk(*s, local, nlocal, 0, s->batch, slab, flags, st)) != ET_OK) return rc;
         const int64_t mine = s->split[s->rank + 1] - s->split[s->rank];
-        if (!s->comm) {
+        if (!s->comm && !s->loop) {
             ET_HIP_CHECK(hipMemcpyAsync(gath, slab, size_t(mine) * row, hipMemcpyDeviceToDevice, st));
         } else {
-            ET_NCCL_CHECK(ncclGroupStart());
+            // rank p gets bags [split[p], split[p+1]) of this slab; this rank receives its
+            // own bag slice of every rank's slab, rank after rank
+            et::LoopPost m;
             for (int p = 0; p < s->world; ++p) {
                 const int64_t n = s->split[p + 1] - s->split[p];
-                ET_NCCL_CHECK(ncclSend(slab + s->split[p] * row, size_t(n) * row, ncclUint8, p, s->comm, st));
-                ET_NCCL_CHECK(ncclRecv(gath + p * mine * row, size_t(mine) * row, ncclUint8, p, s->comm, st));
+                m.send.push_back(slab + s->split[p] * row);
+                m.sbytes.push_back(size_t(n) * row);
+                m.recv.push_back(gath + p * mine * row);
+                m.rbytes.push_back(size_t(mine) * row);
             }
-            ET_NCCL_CHECK(ncclGroupEnd());
+            rc = s->loop ? et::loop_exchange(s->loop, std::move(m), st) : et::nccl_exchange(s->comm, m, st);
+            if (rc != ET_OK) return rc;
         }
         for (auto& L : s->launches)
             if ((rc = et_concat_slabs(s->dtype, gath + L.shift * s->es, s->world, s->slab_ld, mine,
@@ -474,18 +692,19 @@ extern "C" int et_sharded_piece_grads(void* handle, const void* delta, int64_t l
                                  L.offs.data(), send + L.shift * s->es, s->slab_ld, st)) != ET_OK)
             return rc;
     char* out = (char*)recv;  // batch x slab_ld: every bag, this rank's features
-    if (!s->comm) {
+    if (!s->comm && !s->loop) {
         ET_HIP_CHECK(hipMemcpyAsync(out, send, size_t(mine) * row, hipMemcpyDeviceToDevice, st));
         return ET_OK;
     }
-    ET_NCCL_CHECK(ncclGroupStart());
+    et::LoopPost m;
     for (int p = 0; p < s->world; ++p) {
         const int64_t n = s->split[p + 1] - s->split[p];
-        ET_NCCL_CHECK(ncclSend(send + p * mine * row, size_t(mine) * row, ncclUint8, p, s->comm, st));
-        ET_NCCL_CHECK(ncclRecv(out + s->split[p] * row, size_t(n) * row, ncclUint8, p, s->comm, st));
+        m.send.push_back(send + p * mine * row);
+        m.sbytes.push_back(size_t(mine) * row);
+        m.recv.push_back(out + s->split[p] * row);
+        m.rbytes.push_back(size_t(n) * row);
     }
-    ET_NCCL_CHECK(ncclGroupEnd());
-    return ET_OK;
+    return s->loop ? et::loop_exchange(s->loop, std::move(m), st) : et::nccl_exchange(s->comm, m, st);
 }
 
 extern "C" int et_sharded_destroy(void* handle) {

@@ -25,7 +25,7 @@ ET_FLAG_SGD_APPLY_ONLY = 64
 ET_FLAG_SGD_HOT_PASS = 128
 ET_MAX_TABLES_PER_LAUNCH = 32
 ET_SGD_CHUNK = 256  # include/embtab.h: occurrences per chunk of the non-exact SGD
-ET_ABI_VERSION = 6
+ET_ABI_VERSION = 7
 ET_MAX_PEERS = 16
 ET_PLAN_TABLEWISE, ET_PLAN_FEATUREWISE = 0, 1
 ET_EXCHANGE_ALLGATHER, ET_EXCHANGE_ALLTOALL = 0, 1
@@ -63,6 +63,7 @@ EXPORTS = (
     "et_comm_unique_id",
     "et_comm_init",
     "et_comm_destroy",
+    "et_comm_loopback",
     "et_allgather_concat",
     "et_sharded_create",
     "et_sharded_info",
@@ -164,6 +165,7 @@ def load() -> ctypes.CDLL:
         "et_comm_unique_id": ([vp], c_int),
         "et_comm_init": ([vp, i32, vp, i32], c_int),
         "et_comm_destroy": ([vp], c_int),
+        "et_comm_loopback": ([vp, i32], c_int),
         "et_allgather_concat": ([vp, c_int, vp, i64, i64, vp, i32, vp, vp, vp, i64, vp], c_int),
         "et_sharded_create": ([vp, vp, i32, i32, c_int, vp, i32, i64, i64, i64, i32, i32], c_int),
         "et_sharded_info": ([vp, vp, vp, vp, vp], c_int),

@@ -194,7 +194,7 @@ class ShardedMapLookup:
 
     def __init__(self, plan: ShardPlan, rank: int, world: int, batch: int, dtype, device,
                  group=None, exchange: str = "allgather", chunks: int = 1, native=None,
-                 rccl=None):
+                 rccl=None, comm=None):
         if plan.world != world:
             raise ValueError("plan and world size differ")
         if exchange not in ("allgather", "alltoall", "p2p"):
@@ -205,6 +205,8 @@ class ShardedMapLookup:
         self.dtype = dtype
         self._native = None
         auto = native is None
+        if comm is not None:  # a caller-owned communicator (e.g. a loopback rank)
+            native, auto = True, False
         if auto:  # the C-ABI step whenever the ranks are real GPU processes
             native = (exchange != "p2p" and self.device.type == "cuda" and
                       (world == 1 or self._nccl_group()))
@@ -213,7 +215,8 @@ class ShardedMapLookup:
             try:
                 self._native = NativeShardedStep(plan, rank, world, batch, dtype, self.device,
                                                  group, exchange, self.chunks,
-                                                 rccl=world > 1 if rccl is None else rccl)
+                                                 rccl=world > 1 if rccl is None else rccl,
+                                                 comm=comm)
             except _lib.EmbtabError as e:
                 if not auto:
                     raise
@@ -579,31 +582,40 @@ class NativeShardedStep:
     with et_comm_unique_id / et_comm_init, the id broadcast over ``group``."""
 
     def __init__(self, plan: ShardPlan, rank: int, world: int, batch: int, dtype, device,
-                 group=None, exchange: str = "allgather", chunks: int = 1, rccl: bool = True):
+                 group=None, exchange: str = "allgather", chunks: int = 1, rccl: bool = True,
+                 comm=None):
         self.plan, self.rank, self.world, self.batch = plan, rank, world, batch
         self.device, self.exchange = device, exchange
         self.L = L = _lib.load()
         self._et_dtype = _lib.TORCH_TO_ET[dtype]
-        self.comm = ctypes.c_void_p(None)
+        self.comm = ctypes.c_void_p(None)  # owned by this object (made here), else:
+        self._ext_comm = comm              # a caller-owned communicator, never destroyed here
+        self.h = None
         with torch.cuda.device(device):
-            if rccl:
+            if comm is None and rccl:
                 self.comm = make_comm(group, rank, world)
-            flat = [p for r in range(world) for p in plan.pieces[r]]
-            arr = (_lib.ShardPiece * max(1, len(flat)))()
-            for i, (r, p) in enumerate((r, p) for r in range(world) for p in plan.pieces[r]):
-                arr[i] = _lib.ShardPiece(r, p.table, p.f0, p.dim, p.col)
-            h = ctypes.c_void_p()
-            kind = (_lib.ET_EXCHANGE_ALLTOALL if exchange == "alltoall"
-                    else _lib.ET_EXCHANGE_ALLGATHER)
-            _lib.check(L.et_sharded_create(ctypes.byref(h), self.comm, world, rank,
-                                           self._et_dtype, ctypes.addressof(arr), len(flat),
-                                           plan.prependrows, plan.ld, batch, chunks, kind))
-            self.h = h
-            ld, ws, lo, hi = (ctypes.c_int64() for _ in range(4))
-            _lib.check(L.et_sharded_info(h, ctypes.byref(ld), ctypes.byref(ws), ctypes.byref(lo),
-                                         ctypes.byref(hi)))
-            self.slab_ld, self.lo, self.hi = ld.value, lo.value, hi.value
-            self.workspace = torch.empty(ws.value, dtype=torch.uint8, device=device)
+            try:
+                flat = [p for r in range(world) for p in plan.pieces[r]]
+                arr = (_lib.ShardPiece * max(1, len(flat)))()
+                for i, (r, p) in enumerate((r, p) for r in range(world) for p in plan.pieces[r]):
+                    arr[i] = _lib.ShardPiece(r, p.table, p.f0, p.dim, p.col)
+                h = ctypes.c_void_p()
+                kind = (_lib.ET_EXCHANGE_ALLTOALL if exchange == "alltoall"
+                        else _lib.ET_EXCHANGE_ALLGATHER)
+                _lib.check(L.et_sharded_create(ctypes.byref(h), comm if comm is not None
+                                               else self.comm, world, rank, self._et_dtype,
+                                               ctypes.addressof(arr), len(flat),
+                                               plan.prependrows, plan.ld, batch, chunks, kind))
+                self.h = h
+                ld, ws, lo, hi = (ctypes.c_int64() for _ in range(4))
+                _lib.check(L.et_sharded_info(h, ctypes.byref(ld), ctypes.byref(ws),
+                                             ctypes.byref(lo), ctypes.byref(hi)))
+                self.slab_ld, self.lo, self.hi = ld.value, lo.value, hi.value
+                self.workspace = torch.empty(ws.value, dtype=torch.uint8, device=device)
+            except BaseException:
+                # never leak the communicator (or the handle) of a half-made step
+                self.close()
+                raise
         self._descs = {}
 
     def _local_descs(self, piece_tables, piece_idx):
@@ -651,6 +663,18 @@ class NativeShardedStep:
         if self.comm:
             _lib.check(self.L.et_comm_destroy(self.comm))
             self.comm = ctypes.c_void_p(None)
+
+
+def loopback_comms(world: int) -> list:
+    """et_comm_loopback: ``world`` simulated ranks of this process (rank r = item r), all
+    on the current device, for running the world > 1 native step without ``world`` GPUs:
+    drive each rank from its own host thread and stream (ctypes releases the GIL during
+    the calls, so the ranks' collectives rendezvous inside the library).  Free each with
+    ``_lib.load().et_comm_destroy``."""
+    L = _lib.load()
+    arr = (ctypes.c_void_p * world)()
+    _lib.check(L.et_comm_loopback(ctypes.addressof(arr), world))
+    return [ctypes.c_void_p(arr[r]) for r in range(world)]
 
 
 def make_comm(group, rank: int, world: int) -> ctypes.c_void_p:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 6
+#define ET_ABI_VERSION 7
 
 /* Status codes. */
 #define ET_OK 0
@@ -318,6 +318,16 @@ int et_shard_plan(int32_t mode, int32_t ntables, const int32_t* dims, const int6
 int et_comm_unique_id(void* id);
 int et_comm_init(void** comm, int32_t nranks, const void* id, int32_t rank);
 int et_comm_destroy(void* comm);
+
+/* A LOOPBACK communicator: nranks simulated ranks of this one process (comms[r] is rank r),
+ * all on the current device, for exercising the world > 1 sharded step without nranks
+ * GPUs.  Each rank must be driven by its own host thread with its own stream; every
+ * collective of the sharded step (et_sharded_maplookup, et_sharded_piece_grads,
+ * et_allgather_concat) is then a host rendezvous of the nranks callers followed by device
+ * copies between their buffers, stream-ordered with events as RCCL orders its collectives.
+ * Accepted wherever an RCCL comm is (world must equal nranks); a caller that does not
+ * arrive within 120 s fails the collective.  Free each handle with et_comm_destroy. */
+int et_comm_loopback(void** comms, int32_t nranks);
 
 /* The exchange step on its own: ncclAllGather of every rank's (slab_ld x batch) slab into
  * `gathered` (nranks slabs, rank after rank), then et_concat_slabs(gathered, rows,
