@@ -521,8 +521,10 @@ def main():
     dims = [DIM] * T
     sharded = world > 1 or args.force_shard
     if sharded:
+        # table-wise: dealt by size so the 5 tables above 256 MiB land on distinct ranks
+        # (SURVEY.md §8e); counts stay 4,4,3,3,3,3,3,3 at N = 8
         plan = (ShardPlan.featurewise(dims, world) if args.plan == "featurewise"
-                else ShardPlan.tablewise(dims, world))
+                else ShardPlan.tablewise(dims, world, sizes=CRITEO_KAGGLE_ROWS))
         mine = plan.tables_of(rank)
         pieces = plan.pieces[rank]
         tables = []
@@ -632,8 +634,8 @@ def main():
             "parallelism": "single GPU" if not sharded else
                            ("feature-wise: equal contiguous feature ranges per GPU, tables "
                             "cut at 32-feature granules" if args.plan == "featurewise"
-                            else "table-wise: whole tables per GPU, contiguous groups balanced "
-                                 "by count (SURVEY.md §8e)")
+                            else "table-wise: whole tables per GPU, balanced by count and dealt "
+                                 "by size so the largest land on distinct GPUs (SURVEY.md §8e)")
                            + f" x{world} + "
                            f"{'RCCL' if args.backend == 'nccl' else 'gloo'} all-gather concat "
                            f"({shard.chunks} pipelined batch chunks; "
