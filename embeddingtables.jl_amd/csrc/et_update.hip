@@ -1,5 +1,5 @@
 // et_update.hip — fused sparse SGD (Flux.Descent) and the device Indexer for gfx950
-// (included by embtab.hip).
+//
 //
 // Replaces (darchr/EmbeddingTables.jl):
 //   update!(::Descent, table, ::SparseEmbeddingUpdate, indexer, Val)  src/sparseupdate.jl:160-178
@@ -26,6 +26,7 @@
 // the reference's multi-table generic path does), chosen by ET_FLAG_SGD_UNFUSED /
 // ET_FLAG_SGD_F64_ALPHA.
 #include "et_common.h"
+#include "et_chain_asm.h"
 #include "et_sort.hip"
 
 namespace et {
@@ -468,7 +469,8 @@ __device__ __forceinline__ void sgd_chunks_body(
     const UpdatePack& pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, float* __restrict__ partials, int pdim,
-    uint32_t sent, float eta32, double eta64, uint32_t my_mask, int skip_singles) {
+    uint32_t sent, float eta32, double eta64, uint32_t my_mask, int skip_singles,
+    int skip_multi, uint32_t bid, uint32_t nblk) {
     constexpr int VPR = D / 4;
     constexpr int LPR = VPR < 64 ? VPR : 64;
     constexpr int NV = VPR / LPR;
@@ -477,8 +479,8 @@ __device__ __forceinline__ void sgd_chunks_body(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane / LPR, sub = lane % LPR;
     const uint32_t C = counters[kCntC];
-    const uint32_t nwaves = gridDim.x * 4u;
-    const uint32_t wid = blockIdx.x * 4u + wave;
+    const uint32_t nwaves = nblk * 4u;
+    const uint32_t wid = bid * 4u + wave;
     for (uint32_t it = 0; (uint64_t)it * 64u * nwaves + wid < C; ++it) {
         // metadata of chunks (it*64 + l) * nwaves + wid, one per lane l
         const uint64_t cl = ((uint64_t)it * 64u + lane) * nwaves + wid;
@@ -489,8 +491,10 @@ __device__ __forceinline__ void sgd_chunks_body(
         const uint64_t left = ((uint64_t)C - wid + nwaves - 1) / nwaves - (uint64_t)it * 64u;
         uint32_t nq = left < 64u ? (uint32_t)left : 64u;
         if (skip_singles) {
-            // the records this pass walks (not k_sgd_singles'), compacted to the front
-            const bool keep = valid && m_key != sent && !(m_dst == kApply && m_s1 - m_s0 == 1u);
+            // the records this pass walks (not k_sgd_singles', nor the exact mode's chains:
+            // the chunks of multi-chunk columns), compacted to the front
+            const bool keep = valid && m_key != sent && !(m_dst == kApply && m_s1 - m_s0 == 1u) &&
+                              !(skip_multi && m_dst != kApply);
             const uint64_t bal = (uint64_t)__ballot(keep);
             const int nk = __popcll(bal);
             const int rk = __popcll(bal & ((1ull << lane) - 1ull));
@@ -548,14 +552,14 @@ __device__ __forceinline__ void sgd_chunks_body(
 template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chunks(ET_SGD_CHUNKS_ARGS) {
     sgd_chunks_body<D, MODE, NT>(pack, ntables, keys, vals, recs, counters, partials, pdim, sent,
-                                 eta32, eta64, my_mask, skip_singles);
+                                 eta32, eta64, my_mask, skip_singles, 0, blockIdx.x, gridDim.x);
 }
 // The same pass compiled for 5 waves per SIMD (96 VGPRs instead of 97-104: 4 waves).
 template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chunks5(
     ET_SGD_CHUNKS_ARGS) {
     sgd_chunks_body<D, MODE, NT>(pack, ntables, keys, vals, recs, counters, partials, pdim, sent,
-                                 eta32, eta64, my_mask, skip_singles);
+                                 eta32, eta64, my_mask, skip_singles, 0, blockIdx.x, gridDim.x);
 }
 #undef ET_SGD_CHUNKS_ARGS
 
@@ -1068,6 +1072,384 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
     store_scalar<NT>(w + 1, sgd_apply<MODE>(w[1], ay, eta32, eta64));
 }
 
+// ---------------------------------------------------------------------------
+// Exact Float32 update: serial chains (ET_FLAG_EXACT_UPDATE)
+// ---------------------------------------------------------------------------
+// The reference sums every distinct column's gradient serially in occurrence order
+// (src/sparseupdate.jl:110-127: acc += delta[:, map[t]] for t in the column's range).
+// Columns with at most kChunk occurrences are one chunk of the chunk pass, which is that
+// serial sum already; the longer ("chain") columns — the multi-chunk list of the split
+// mode — are summed by one wave per 64-feature slice walking the column's run-length
+// list: a run of r occurrences in one bag adds the same delta column r times, so the
+// index phase cuts every run into entries of at most S adds (S per column, the cheapest
+// of 1/2/4/8/16 for its run lengths) and the wave spends exactly S masked fmas per entry
+// in the hand-scheduled loop of et_chain_asm.h (no branch and no memory access per add
+// beyond the delta load; tools/gen_chain_asm.py).  Same additions in the same order as
+// the reference: bit-identical, and no partial sums to combine.
+//
+// Index phase: k_chain_count (run lengths -> S and the entry count per column),
+// k_chain_plan (entry offsets, columns ordered by cost so the longest chains are
+// dispatched first), k_chain_emit (the entries).  Update phase: the chain role of
+// k_sgd_exact, beside the chunk pass (single-chunk columns) and the singles in ONE
+// launch, so the hottest chains (834,828 adds on the config-4 batch) overlap the rest.
+constexpr int kChainGroup = 24;  // entries per trip of the asm loop (3 batches of 8)
+constexpr int kChainPad = 16;    // readable entries past the last trip (its prefetches)
+constexpr int kChainEntryCost = 5;  // per-entry work besides the S fmas (gpr-idx, address,
+                                    // load, wait), in VALU issue slots
+
+struct ChainCol {
+    uint32_t key, e0, ngr, S;  // S == 0: no chain (out-of-range occurrences)
+};
+
+__device__ __forceinline__ uint32_t cdiv_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, int lane) {
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += t;
+    }
+    return x - v;
+}
+
+// Runs of equal bags in a column's sorted occurrences, one 64-occurrence slice at a
+// time.  Per lane: the run starting at this lane if it ends inside the slice.  Uniform:
+// the run carried in from earlier slices if it ends here.  The last run that starts in
+// the slice is carried out (open_start / open_bag, ~0u when there is none).
+struct SliceRuns {
+    bool lane_closed;
+    uint32_t lane_r, lane_bag;
+    bool open_closed;
+    uint32_t open_r, open_bag;
+};
+
+__device__ __forceinline__ SliceRuns slice_runs(const uint32_t* __restrict__ vals, uint32_t c0,
+                                                uint32_t se, uint32_t occ_off, uint32_t pool,
+                                                uint32_t& open_start, uint32_t& open_bag) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t pos = c0 + (uint32_t)lane;
+    const bool valid = pos < se;
+    const uint32_t bag = valid ? (vals[pos] - occ_off) / pool : 0xffffffffu;
+    const uint32_t prev = (uint32_t)__shfl_up((int)bag, 1, 64);
+    const bool head = valid && (lane == 0 ? (open_start == 0xffffffffu || bag != open_bag)
+                                          : bag != prev);
+    const uint64_t hm = (uint64_t)__ballot(head);
+    const uint64_t after = lane < 63 ? hm >> (lane + 1) : 0ull;
+    SliceRuns s;
+    s.lane_closed = head && after != 0ull;
+    s.lane_r = after ? (uint32_t)__ffsll((long long)after) : 0u;  // next head - this lane
+    s.lane_bag = bag;
+    s.open_closed = open_start != 0xffffffffu && hm != 0ull;
+    s.open_r = s.open_closed ? c0 + (uint32_t)(__ffsll((long long)hm) - 1) - open_start : 0u;
+    s.open_bag = open_bag;
+    if (hm != 0ull) {
+        const int last = 63 - __clzll((long long)hm);
+        open_start = c0 + (uint32_t)last;
+        open_bag = (uint32_t)__shfl((int)bag, last, 64);
+    }
+    return s;
+}
+
+// Index phase 1: per chain column, S and the padded entry count.
+__global__ __launch_bounds__(256) void k_chain_count(UpdatePack pack, int ntables,
+                                                     const uint32_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ vals,
+                                                     const uint32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ mlist,
+                                                     const uint32_t* __restrict__ counters,
+                                                     uint32_t sent, uint32_t* __restrict__ cnt,
+                                                     uint2* __restrict__ info) {
+    const uint32_t M = counters[kCntM];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
+        const uint32_t u = mlist[m];
+        const uint32_t ss = seg_start[u], se = seg_start[u + 1], key = keys[ss];
+        if (key == sent) {
+            if (lane == 0) cnt[m] = 0, info[m] = make_uint2(0u, 0u);
+            continue;
+        }
+        const int t = table_of_key(pack, ntables, key);
+        const uint32_t occ_off = pack.occ_off[t], pool = (uint32_t)pack.d[t].pool;
+        uint32_t E[5] = {se - ss, 0u, 0u, 0u, 0u};  // entries at S = 1, 2, 4, 8, 16
+        uint32_t open_start = 0xffffffffu, open_bag = 0u;
+        for (uint32_t c0 = ss; c0 < se; c0 += 64) {
+            const SliceRuns sr = slice_runs(vals, c0, se, occ_off, pool, open_start, open_bag);
+            const uint32_t r = sr.lane_r;
+            // per-slice sums of ceil(r/S) over at most 64 occurrences fit 8 bits each
+            const uint32_t pk = sr.lane_closed ? (cdiv_u32(r, 2) | cdiv_u32(r, 4) << 8 |
+                                                  cdiv_u32(r, 8) << 16 | cdiv_u32(r, 16) << 24)
+                                               : 0u;
+            const uint32_t tot = wave_sum_u32(pk);
+#pragma unroll
+            for (int k = 1; k < 5; ++k) E[k] += (tot >> (8 * (k - 1))) & 0xffu;
+            if (sr.open_closed)
+#pragma unroll
+                for (int k = 1; k < 5; ++k) E[k] += cdiv_u32(sr.open_r, 1u << k);
+        }
+        {
+            const uint32_t r = se - open_start;  // the last run
+#pragma unroll
+            for (int k = 1; k < 5; ++k) E[k] += cdiv_u32(r, 1u << k);
+        }
+        int best = 0;
+        uint64_t bc = ~0ull;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint64_t c = (uint64_t)E[k] * (uint64_t)((1 << k) + kChainEntryCost);
+            if (c < bc) bc = c, best = k;
+        }
+        if (lane == 0) {
+            cnt[m] = cdiv_u32(E[best], kChainGroup) * kChainGroup + kChainPad;
+            info[m] = make_uint2(1u << best, E[best]);
+        }
+    }
+}
+
+// Inclusive scan of one value per thread over a 1024-thread workgroup.
+__device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32_t* lds16,
+                                                              uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) lds16[wave] = v;
+    __syncthreads();
+    uint32_t off = 0, all = 0;
+    for (int w = 0; w < 16; ++w) {
+        off += w < wave ? lds16[w] : 0u;
+        all += lds16[w];
+    }
+    *total = all;
+    __syncthreads();
+    return v + off;
+}
+
+// Index phase 2 (one workgroup): entry offsets (exclusive scan of the padded counts) and
+// the dispatch order: columns bucketed by log2 of their cost (entries x (S + overhead)),
+// costliest bucket first; the order inside a bucket is arbitrary (results never depend
+// on which wave takes a column).
+__global__ __launch_bounds__(1024) void k_chain_plan(const uint32_t* __restrict__ counters,
+                                                     const uint32_t* __restrict__ cnt,
+                                                     const uint2* __restrict__ info,
+                                                     uint32_t* __restrict__ e0,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t lds16[16];
+    __shared__ uint32_t hist[65];
+    const uint32_t M = counters[kCntM];
+    if (threadIdx.x < 65) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    auto bucket = [&](uint32_t m) {  // leading zeros of the cost: 0 = costliest, 64 = none
+        const uint2 in = info[m];
+        const uint64_t c = (uint64_t)in.y * (uint64_t)(in.x + kChainEntryCost);
+        return c ? (uint32_t)__clzll((long long)c) : 64u;
+    };
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < M; b0 += 1024) {
+        const uint32_t m = b0 + threadIdx.x;
+        const uint32_t v = m < M ? cnt[m] : 0u;
+        uint32_t total;
+        const uint32_t inc = block_inclusive_scan_1024(v, lds16, &total);
+        if (m < M) {
+            e0[m] = carry + inc - v;
+            atomicAdd(&hist[bucket(m)], 1u);
+        }
+        carry += total;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < 65; ++k) {
+            const uint32_t h = hist[k];
+            hist[k] = run;
+            run += h;
+        }
+    }
+    __syncthreads();
+    for (uint32_t m = threadIdx.x; m < M; m += 1024) {
+        order[atomicAdd(&hist[bucket(m)], 1u)] = m;
+    }
+}
+
+// One run of r adds of delta column `bag` as ceil(r/S) entries (S adds each, the last
+// one the remainder): (delta element offset, S - adds).
+__device__ __forceinline__ void chain_put(uint2* __restrict__ ent, uint32_t at, uint32_t i,
+                                          uint32_t k, uint32_t r, uint32_t S, uint32_t off) {
+    const uint32_t adds = i + 1 < k ? S : r - S * (k - 1);
+    ent[at] = make_uint2(off, S - adds);
+}
+
+// Index phase 3: the entries, padded with (0, S) (masks all zero) to the planned count.
+__global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables,
+                                                    const uint32_t* __restrict__ keys,
+                                                    const uint32_t* __restrict__ vals,
+                                                    const uint32_t* __restrict__ seg_start,
+                                                    const uint32_t* __restrict__ mlist,
+                                                    const uint32_t* __restrict__ counters,
+                                                    const uint32_t* __restrict__ cnt,
+                                                    const uint2* __restrict__ info,
+                                                    const uint32_t* __restrict__ e0s,
+                                                    uint2* __restrict__ ent,
+                                                    ChainCol* __restrict__ chains) {
+    const uint32_t M = counters[kCntM];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
+        const uint32_t P = cnt[m];
+        const uint32_t u = mlist[m];
+        const uint32_t ss = seg_start[u], se = seg_start[u + 1], key = keys[ss];
+        if (P == 0) {
+            if (lane == 0) chains[m] = ChainCol{key, 0u, 0u, 0u};
+            continue;
+        }
+        const uint32_t S = info[m].x, e0 = e0s[m];
+        const int t = table_of_key(pack, ntables, key);
+        const uint32_t occ_off = pack.occ_off[t], pool = (uint32_t)pack.d[t].pool;
+        const uint32_t ld = (uint32_t)pack.d[t].ld_delta;
+        uint32_t at = e0;
+        uint32_t open_start = 0xffffffffu, open_bag = 0u;
+        for (uint32_t c0 = ss; c0 < se; c0 += 64) {
+            const SliceRuns sr = slice_runs(vals, c0, se, occ_off, pool, open_start, open_bag);
+            if (sr.open_closed) {  // the carried run precedes this slice's runs
+                const uint32_t k = cdiv_u32(sr.open_r, S);
+                for (uint32_t i = lane; i < k; i += 64)
+                    chain_put(ent, at + i, i, k, sr.open_r, S, sr.open_bag * ld);
+                at += k;
+            }
+            const uint32_t k = sr.lane_closed ? cdiv_u32(sr.lane_r, S) : 0u;
+            const uint32_t pre = wave_excl_scan_u32(k, lane);
+            for (uint32_t i = 0; i < k; ++i)
+                chain_put(ent, at + pre + i, i, k, sr.lane_r, S, sr.lane_bag * ld);
+            at += (uint32_t)__shfl((int)(pre + k), 63, 64);
+        }
+        {
+            const uint32_t r = se - open_start, k = cdiv_u32(r, S);
+            for (uint32_t i = lane; i < k; i += 64) chain_put(ent, at + i, i, k, r, S, open_bag * ld);
+            at += k;
+        }
+        for (uint32_t i = at + lane; i < e0 + P; i += 64) ent[i] = make_uint2(0u, S);
+        if (lane == 0) chains[m] = ChainCol{key, e0, (P - kChainPad) / kChainGroup, S};
+    }
+}
+
+// Debug check of the chain plan (ET_CHAIN_CHECK=1): every entry of every chain addresses
+// a gradient column of its table's batch with a mask index <= S, the entries carrying
+// adds number exactly E and precede the padding; a violation is counted in the device
+// error word (et_check_errors) as 1 << 20 and the entry neutralised to (0, S).
+__global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntables,
+                                                     const uint32_t* __restrict__ counters,
+                                                     const uint32_t* __restrict__ cnt,
+                                                     const uint2* __restrict__ info,
+                                                     uint2* __restrict__ ent,
+                                                     const ChainCol* __restrict__ chains,
+                                                     const uint32_t* __restrict__ order) {
+    const uint32_t M = counters[kCntM];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < M; i += gridDim.x * 256)
+        if (order[i] >= M) note_oob(1 << 22);
+    for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
+        const ChainCol c = chains[m];
+        const uint32_t P = cnt[m];
+        if (c.S == 0u) continue;
+        const int t = table_of_key(pack, ntables, c.key);
+        const uint64_t lim = (uint64_t)pack.d[t].batch * (uint64_t)pack.d[t].ld_delta;
+        uint32_t bad = 0, real = 0, pad_then_real = 0;
+        if (P != c.ngr * kChainGroup + kChainPad || c.S != info[m].x) bad = 1;
+        for (uint32_t i = lane; i < P; i += 64) {
+            const uint2 e = ent[c.e0 + i];
+            const bool ok = (uint64_t)e.x < lim && e.y <= c.S;
+            if (!ok) ent[c.e0 + i] = make_uint2(0u, c.S);
+            bad += ok ? 0u : 1u;
+            real += (ok && e.y < c.S) ? 1u : 0u;
+            pad_then_real += (ok && e.y < c.S && i >= info[m].y) ? 1u : 0u;
+        }
+        bad = wave_sum_u32(bad) + wave_sum_u32(pad_then_real);
+        real = wave_sum_u32(real);
+        if (lane == 0 && (bad || real != info[m].y)) note_oob(1 << 20);
+    }
+}
+
+// Update phase, chain role: wave w takes items w, w + nwaves, ... of the cost-ordered
+// (column, 64-feature slice) list and applies the update of its slice.
+template <int MODE, bool NT>
+__device__ __forceinline__ void sgd_chain_body(const UpdatePack& pack, int ntables,
+                                               const uint32_t* __restrict__ counters,
+                                               const ChainCol* __restrict__ chains,
+                                               const uint32_t* __restrict__ order,
+                                               const uint2* __restrict__ ent, int ns,
+                                               float eta32, double eta64, uint32_t bid,
+                                               uint32_t nblk, bool plain) {
+    const int lane = threadIdx.x & 63;
+    // wave-uniform by construction; readfirstlane lets the compiler keep everything
+    // derived from it (the chain's entry pointer, its count) in SGPRs, as the asm needs
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t M = counters[kCntM];
+    const uint32_t nw = nblk * 4u, items = M * (uint32_t)ns;
+    for (uint32_t it = bid * 4u + (uint32_t)wave; it < items; it += nw) {
+        const ChainCol c = chains[order[it / (uint32_t)ns]];
+        if (c.S == 0u) continue;
+        const int t = table_of_key(pack, ntables, c.key);
+        const et_update_desc& d = pack.d[t];
+        const int f = (int)(it % (uint32_t)ns) * 64 + lane;
+        if ((int)(it % (uint32_t)ns) * 64 >= d.dim) continue;  // uniform
+        const float* xb = reinterpret_cast<const float*>(d.delta) + (f < d.dim ? f : d.dim - 1);
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(ent + c.e0);
+        float acc = 0.0f;
+        if (plain) {  // debug reference of the asm loop: the same adds, plainly
+            const uint32_t ne = c.ngr * kChainGroup;
+            for (uint32_t h = 0; h < ne; ++h) {
+                const uint2 en = ent[c.e0 + h];
+                const float x = xb[en.x];
+                for (uint32_t k = en.y; k < c.S; ++k) acc = acc + x;
+            }
+        } else
+        switch (c.S) {
+            case 1: acc = chain_walk_asm<1>(e, c.ngr, xb, 0.0f); break;
+            case 2: acc = chain_walk_asm<2>(e, c.ngr, xb, 0.0f); break;
+            case 4: acc = chain_walk_asm<4>(e, c.ngr, xb, 0.0f); break;
+            case 8: acc = chain_walk_asm<8>(e, c.ngr, xb, 0.0f); break;
+            default: acc = chain_walk_asm<16>(e, c.ngr, xb, 0.0f); break;
+        }
+        if (f < d.dim) {
+            float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
+            store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+        }
+    }
+}
+
+// The whole update phase of an exact Float32 call in one launch: blocks [0, ncb) the
+// chains, [ncb, ncb + nch) the chunk pass over single-chunk columns of this capacity
+// group, the rest the single-occurrence columns.  D == 0: chains only (no vector table).
+template <int D, int MODE, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_exact(
+    UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
+    const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
+    const uint32_t* __restrict__ counters, uint32_t sent, float eta32, double eta64,
+    uint32_t my_mask, const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
+    const uint2* __restrict__ ent, int ns, uint32_t ncb, uint32_t nch, int plain) {
+    if (blockIdx.x < ncb) {
+        sgd_chain_body<MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta32, eta64,
+                                 blockIdx.x, ncb, plain != 0);
+        return;
+    }
+    if constexpr (D > 0) {
+        if (blockIdx.x < ncb + nch)
+            sgd_chunks_body<D, MODE, NT>(pack, ntables, keys, vals, recs, counters, nullptr, 0,
+                                         sent, eta32, eta64, my_mask, 1, 1, blockIdx.x - ncb, nch);
+        else
+            sgd_singles_body<D, MODE, NT>(pack, ntables, vals, recs, counters, sent, eta32, eta64,
+                                          my_mask, blockIdx.x - ncb - nch,
+                                          gridDim.x - ncb - nch);
+    }
+}
+
 // Generic kernels (any dim / alignment / element type): one wave per chunk or
 // combined segment, lanes over features, scalar loads.  T is the table and gradient
 // type, C the accumulator (sgd_apply_t).
@@ -1076,14 +1458,14 @@ __global__ __launch_bounds__(256) void k_sgd_chunks_generic(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, C* __restrict__ partials, int pdim, uint32_t sent,
-    C eta_c, double eta64) {
+    C eta_c, double eta64, int skip_multi) {
     const int lane = threadIdx.x & 63;
     const uint32_t Cn = counters[kCntC];
     const uint32_t waves = gridDim.x * 4;
     for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < Cn; c += waves) {
         const ChunkRec r = recs[c];
         const uint32_t key = r.key;
-        if (key == sent) continue;
+        if (key == sent || (skip_multi && r.dst != kApply)) continue;  // (chains: exact F32)
         const int t = table_of_key(pack, ntables, key);
         const et_update_desc& d = pack.d[t];
         if ((pack.vec_mask >> t) & 1u) continue;  // handled by the vector kernel
@@ -1156,6 +1538,13 @@ struct UpdateWs {
     float2* hot_part;
     uint8_t* hot_slots;  // [sum over hot-shaped tables of batch * roundup(pool, 4)]
     int hot_nw;
+    // exact Float32 mode: chain entries (aliasing `partials`: that mode has no partial
+    // sums), per chain column (multi-chunk list slot) its descriptor, padded entry count,
+    // (S, entries), entry offset, and the cost-ordered slot list
+    uint2* chain_ent;
+    ChainCol* chains;
+    uint32_t *chain_cnt, *chain_e0, *chain_order;
+    uint2* chain_info;
     int64_t bytes;
 };
 
@@ -1192,8 +1581,18 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
     w.counters = (uint32_t*)take(4 * kCntSlots);
     w.mlist = (uint32_t*)take(4 * (n / chunk + 2));
     const int64_t max_partials = 2 * (n / chunk) + 2;
-    // 8 bytes per partial element: float (vector path / fp32 accumulators) or double
-    w.partials = (float*)take(8 * max_partials * (int64_t)(pdim > 0 ? pdim : 1));
+    const int64_t mmax = n / chunk + 2;  // multi-chunk (chain) columns
+    // 8 bytes per partial element: float (vector path / fp32 accumulators) or double; the
+    // exact mode's chain entries (8 bytes, at most one per occurrence + padding) alias it
+    const int64_t part_b = 8 * max_partials * (int64_t)(pdim > 0 ? pdim : 1);
+    const int64_t chain_b = 8 * (n + (int64_t)(kChainGroup + kChainPad) * mmax + 64);
+    w.partials = (float*)take(part_b > chain_b ? part_b : chain_b);
+    w.chain_ent = (uint2*)w.partials;
+    w.chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * mmax);
+    w.chain_cnt = (uint32_t*)take(4 * mmax);
+    w.chain_e0 = (uint32_t*)take(4 * mmax);
+    w.chain_order = (uint32_t*)take(4 * mmax);
+    w.chain_info = (uint2*)take(8 * mmax);
     w.hot_nw = (int)((hot_batch + kHotWin - 1) / kHotWin);
     w.hot_hist = nullptr;
     w.hot_cnt = nullptr;
@@ -1238,7 +1637,8 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
 
 inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s,
-                             uint32_t hot_mask = 0, const HotList* hl = nullptr) {
+                             uint32_t hot_mask = 0, const HotList* hl = nullptr,
+                             bool chain = false) {
     const int64_t blocks = cdiv64(n, 256);
     const unsigned kb_grid = (unsigned)(blocks < 65536 ? blocks : 65536);
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
@@ -1297,6 +1697,26 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chunk_records_multi, dim3(512), dim3(256), 0, s, w.nch, w.seg_start,
                        w.multi, out.keys, w.mlist, chunk, w.counters, w.recs);
     ET_LAUNCH_CHECK("k_chunk_records");
+    if (chain) {  // exact Float32 mode: the multi-chunk columns become serial chains
+        const int64_t mmax = n / chunk + 2;
+        const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
+        hipLaunchKernelGGL(k_chain_count, dim3(cg), dim3(256), 0, s, pack, ntables, out.keys,
+                           out.vals, w.seg_start, w.mlist, w.counters, sent, w.chain_cnt,
+                           w.chain_info);
+        hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
+                           w.chain_info, w.chain_e0, w.chain_order);
+        hipLaunchKernelGGL(k_chain_emit, dim3(cg), dim3(256), 0, s, pack, ntables, out.keys,
+                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_cnt, w.chain_info,
+                           w.chain_e0, w.chain_ent, w.chains);
+        ET_LAUNCH_CHECK("k_chain_emit");
+        static const bool check = [] {
+            const char* e = getenv("ET_CHAIN_CHECK");
+            return e && atoi(e) != 0;
+        }();
+        if (check)
+            hipLaunchKernelGGL(k_chain_check, dim3(cg), dim3(256), 0, s, pack, ntables, w.counters,
+                               w.chain_cnt, w.chain_info, w.chain_ent, w.chains, w.chain_order);
+    }
     if (hot_mask && w.hot_hist && hl && hl->n > 0) {
         ET_HIP_CHECK(hipMemsetAsync(w.hot_hist, 0, 4 * (32 * 32 + 32), s));
         hipLaunchKernelGGL(k_hot_hist, dim3(256), dim3(256), 0, s, pack, ntables, hot_mask,
@@ -1352,12 +1772,72 @@ inline bool sgd_chunks_occ5() {
     return v;
 }
 
+// Workgroups of the exact mode's chain role: one item per (chain column, 64-feature slice),
+// cost-ordered; 512 workgroups (2048 waves) cover the ~17 K items of the config-4 batch in
+// about eight rounds, the first round holding the longest chains.
+inline unsigned chain_blocks(int64_t n) {
+    const int64_t g = cdiv64(n, 65536);
+    return (unsigned)(g < 1 ? 1 : g > 512 ? 512 : g);
+}
+
+// The update phase of an exact Float32 call: chains + chunk pass + singles in one launch
+// per capacity group (the chains ride in the first), then the generic tables' single-chunk
+// columns.  No partial sums, no combine.
+template <int MODE, bool NT>
+int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
+                     int64_t n, int pdim, uint32_t sent, float eta32, double eta64,
+                     const VecGroups& vg, bool any_generic, hipStream_t s, unsigned grid) {
+    const unsigned ncb = chain_blocks(n);
+    const int ns = (pdim + 63) / 64;
+    static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++
+        const char* e = getenv("ET_CHAIN_ASM");
+        return e && atoi(e) == 0 ? 1 : 0;
+    }();
+    if (vg.n == 0)
+        hipLaunchKernelGGL((k_sgd_exact<0, MODE, NT>), dim3(ncb), dim3(256), 0, s, pack, ntables,
+                           gr.keys, gr.vals, w.recs, w.counters, sent, eta32, eta64, 0u, w.chains,
+                           w.chain_order, w.chain_ent, ns, ncb, 0u, plain);
+#define ET_SGD_EXACT(DD)                                                                       \
+    case DD:                                                                                   \
+        hipLaunchKernelGGL((k_sgd_exact<DD, MODE, NT>), dim3(nc + 2 * grid), dim3(256), 0, s,  \
+                           pack, ntables, gr.keys, gr.vals, w.recs, w.counters, sent, eta32,   \
+                           eta64, vg.mask[i], w.chains, w.chain_order, w.chain_ent, ns, nc,    \
+                           grid, plain);                                                       \
+        break;
+    for (int i = 0; i < vg.n; ++i) {
+        const unsigned nc = i == 0 ? ncb : 0u;
+        switch (vg.cap[i]) {
+            ET_SGD_EXACT(16)
+            ET_SGD_EXACT(32)
+            ET_SGD_EXACT(64)
+            ET_SGD_EXACT(128)
+            ET_SGD_EXACT(256)
+            ET_SGD_EXACT(512)
+            ET_SGD_EXACT(1024)
+            ET_SGD_EXACT(2048)
+            default: break;
+        }
+    }
+#undef ET_SGD_EXACT
+    ET_LAUNCH_CHECK("k_sgd_exact");
+    if (any_generic) {
+        hipLaunchKernelGGL((k_sgd_chunks_generic<float, float, MODE, NT>), dim3(grid), dim3(256),
+                           0, s, pack, ntables, gr.keys, gr.vals, w.recs, w.counters, w.partials,
+                           pdim, sent, eta32, eta64, 1);
+        ET_LAUNCH_CHECK("k_sgd_chunks_generic");
+    }
+    return ET_OK;
+}
+
 template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
                      const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl, unsigned grid) {
+                     const HotList& hl, unsigned grid, bool chain, int64_t n) {
     if constexpr (__is_same(T, float)) {
+        if (chain)
+            return launch_sgd_exact<MODE, NT>(pack, ntables, gr, w, n, pdim, sent, eta_c, eta64, vg,
+                                              any_generic, s, grid);
         const bool singles = sgd_singles();
         // combine workgroups of k_sgd_tail: a quarter of one resident wave of workgroups,
         // so the singles start at once beside them
@@ -1411,7 +1891,7 @@ int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         C* partials = reinterpret_cast<C*>(w.partials);
         hipLaunchKernelGGL((k_sgd_chunks_generic<T, C, MODE, NT>), dim3(grid), dim3(256), 0, s,
                            pack, ntables, gr.keys, gr.vals, w.recs, w.counters, partials, pdim,
-                           sent, eta_c, eta64);
+                           sent, eta_c, eta64, 0);
         hipLaunchKernelGGL((k_sgd_combine_generic<T, C, MODE, NT>), dim3(grid), dim3(256), 0, s,
                            pack, ntables, gr.keys, w.seg_start, w.multi, w.counters, partials,
                            pdim, sent, eta_c, eta64);
@@ -1442,10 +1922,10 @@ template <typename T, typename C>
 int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, double eta_c, double eta64,
                      int mode, bool nt, const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl, unsigned grid) {
+                     const HotList& hl, unsigned grid, bool chain = false, int64_t n = 0) {
 #define ET_SGD_CALL(M, NTV)                                                                \
     return launch_sgd_typed<T, C, M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, (C)eta_c, \
-                                          eta64, vg, any_generic, s, hl, grid)
+                                          eta64, vg, any_generic, s, hl, grid, chain, n)
     if (mode == 0) {
         if (nt) ET_SGD_CALL(0, true);
         ET_SGD_CALL(0, false);
@@ -1562,8 +2042,14 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     if (n == 0) return ET_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool exact = (flags & ET_FLAG_EXACT_UPDATE) != 0;
-    // In exact mode a chunk spans a whole segment (n occurrences at most).
-    const uint32_t chunk = exact ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff) : et::kChunk;
+    // Exact Float32: columns longer than a chunk are summed as serial chains (k_chain_*,
+    // k_sgd_exact), which address a gradient column by a 32-bit element offset.  Other
+    // exact calls keep every column in one chunk (a chunk spans a whole segment).
+    bool chain = exact && dtype == ET_F32;
+    for (int t = 0; t < ntables && chain; ++t)
+        if ((uint64_t)descs[t].batch * (uint64_t)descs[t].ld_delta >= 0xffffffffull) chain = false;
+    const uint32_t chunk =
+        exact && !chain ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff) : et::kChunk;
     int nhot;
     int64_t hb, hbytes;
     uint64_t soff[ET_MAX_TABLES_PER_LAUNCH];
@@ -1625,7 +2111,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     if (apply_only) {
         gr = et::grouped_pairs(pack, ntables, w);  // phase 1 ran earlier in stream order
     } else {
-        rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s, hot_mask, &hl);
+        rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s, hot_mask, &hl, chain);
         if (rc != ET_OK || index_only) return rc;
     }
 
@@ -1637,7 +2123,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         case ET_F32:
             return et::launch_sgd_dtype<float, float>(pack, ntables, gr, w, chunk, pdim, sent,
                                                       eta_c, eta, mode, nt, vg,
-                                                      any_generic, s, hl, grid);
+                                                      any_generic, s, hl, grid, chain, n);
         case ET_F64:
             return et::launch_sgd_dtype<double, double>(pack, ntables, gr, w, chunk, pdim, sent,
                                                          eta_c, eta, mode, nt, vg,

@@ -317,7 +317,7 @@ class SplitEmbedding(AbstractEmbeddingTable):
         return self.matrixsize[1]
 
     def _page_col(self, i: int):
-        """``_divrem_index(i, shardsize)`` (src/split.jl:54-60), 0-based page/column."""
+        """``_divrem_index(i, shardsize)`` (src/split.jl:59-65), 0-based page/column."""
         return divmod(i - 1, self.matrixsize[1])
 
     def columnpointer(self, i: int, ctx: IndexingContext | None = None) -> int:

@@ -145,9 +145,12 @@ class Indexer(AbstractIndexer):
     def _defer(self, indices, maxindex: int):
         """The multi-table ``update!`` fills every ``indexers[i]`` in its index phase
         (src/sparseupdate.jl:210-213).  The device update indexes all tables in its own
-        fused pipeline, so the reference-layout Indexer is built from the same index
-        array on first use (et_index_build) instead of on every step."""
-        self._pending = (indices, int(maxindex))
+        fused pipeline, so the reference-layout Indexer is built on first use
+        (et_index_build) instead of on every step — from a stream-ordered SNAPSHOT of the
+        index array taken at update time, so a caller that refills the index buffer in
+        place before reading ``indexers[i]`` still gets the Indexer of the indices this
+        update used (one device copy of the indices: 272 MB, ~0.1 ms at config 4)."""
+        self._pending = (indices.clone(), int(maxindex))
 
     def _materialise(self):
         if self._pending is not None:
@@ -249,6 +252,15 @@ def gettranslations(indexer: AbstractIndexer):
 # --- update! ------------------------------------------------------------------------------------
 
 _UPDATE_DTYPES = (torch.float32, torch.float64, torch.float16, torch.bfloat16)
+
+
+def _hot_pass_ok(descs) -> bool:
+    """The hot-column pass reads gradients with 16-byte vector loads: every gradient of the
+    group must be 16-byte aligned with a leading dimension that is a multiple of 4 (a
+    Preallocation gradient with prependrows not a multiple of 4 is not).  The index phase
+    plans the pass from the tables alone, so the host drops the flag for such a group
+    rather than letting the update phase refuse it."""
+    return all(d.delta % 16 == 0 and d.ld_delta % 4 == 0 for d in descs if d.delta)
 
 
 def _sgd_flags(fused: bool, nontemporal: bool, f64_alpha: bool = False, exact: bool = False,
@@ -378,9 +390,10 @@ def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
         L = _lib.load()
         stream = _lib.stream_handle(dev)
         for (fused, dtype), descs in groups.items():
-            flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc, hot_pass)
             for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
                 part = descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH]
+                flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc,
+                                   hot_pass and _hot_pass_ok(part))
                 arr = (_lib.UpdateDesc * len(part))(*part)
                 nb = ctypes.c_int64(0)
                 _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), len(part),
@@ -455,9 +468,10 @@ class PhasedUpdate:
         self._calls = []  # (dtype, desc array, n, flags, workspace)
         L = _lib.load()
         for (fused, dtype), descs in groups.items():
-            flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc, hot_pass)
             for c in range(0, len(descs), _lib.ET_MAX_TABLES_PER_LAUNCH):
                 part = descs[c:c + _lib.ET_MAX_TABLES_PER_LAUNCH]
+                flags = _sgd_flags(fused, nontemporal, not fused, exact, f16_fp32_acc,
+                                   hot_pass and _hot_pass_ok(part))
                 arr = (_lib.UpdateDesc * len(part))(*part)
                 nb = ctypes.c_int64(0)
                 _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), len(part),

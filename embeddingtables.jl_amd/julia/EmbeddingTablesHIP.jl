@@ -14,7 +14,7 @@
 module EmbeddingTablesHIP
 
 using EmbeddingTables
-import EmbeddingTables: lookup!, maplookup!, update!, columnpointer, example, featuresize
+import EmbeddingTables: lookup!, maplookup!, update!, index!, columnpointer, example, featuresize
 using EmbeddingTables: AbstractEmbeddingTable, Static, Dynamic, SparseEmbeddingUpdate,
     PreallocationStrategy, AbstractIndexer, Indexer
 import Flux
@@ -24,6 +24,7 @@ const libhip = "libamdhip64.so"
 
 const ET_F32, ET_F16, ET_F64, ET_I32, ET_I64 = Cint(0), Cint(1), Cint(2), Cint(3), Cint(4)
 const ET_FLAG_NONTEMPORAL = UInt32(1)
+const ET_FLAG_EXACT_UPDATE = UInt32(4)      # every column summed serially (bit-identical)
 const ET_FLAG_SGD_UNFUSED = UInt32(8)
 const ET_FLAG_SGD_F64_ALPHA = UInt32(16)
 const ET_FLAG_SGD_INDEX_ONLY = UInt32(32)   # phase 1 of update!: index all (src/sparseupdate.jl:210-213)
@@ -332,29 +333,93 @@ function _sparse_sgd(::Type{T}, descs::Vector{UpdateDesc}, eta::Float64, flags::
                 et_dtype(T), descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
 end
 
+# The exact update (ET_FLAG_EXACT_UPDATE, every column's gradient summed serially in the
+# reference's order) is the default; exact = false selects the split mode (long columns
+# summed as ordered partial sums: deterministic, not bit-identical).
+const EXACT = Ref(true)
+
 function update!(opt::Flux.Descent, table::HipTable{S,T}, grad::SparseEmbeddingUpdate,
                  indexer = Indexer(), ::Val{Nontemporal} = Val(true),
-                 args...) where {S,T<:UpdateEltype,Nontemporal}
+                 args...; exact::Bool = EXACT[]) where {S,T<:UpdateEltype,Nontemporal}
     flags = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
-            (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED)
+            (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED) |
+            (exact ? ET_FLAG_EXACT_UPDATE : UInt32(0))
     # convert(eltype(table), opt.eta) happens inside the library
     _sparse_sgd(T, [_update_desc(table, grad)], Float64(opt.eta), flags)
+    return nothing
+end
+
+#####
+##### The Indexer on the device (et_index_build): the reference's cumulative / map layout
+##### (src/utils.jl:280-314) in device arrays, so filling indexers[i] costs no host work
+#####
+
+mutable struct HipIndexer <: AbstractIndexer
+    cumulative_col::Union{Nothing,HipVector{Int64}}  # (col, offset) pairs in first-seen
+    cumulative_off::Union{Nothing,HipVector{Int64}}  # order, then the terminator (0, n+1)
+    map::Union{Nothing,HipVector{Int64}}             # gradient column of each occurrence
+    nunique_dev::Union{Nothing,HipVector{Int64}}
+    workspace::Union{Nothing,HipVector{UInt8}}
+end
+HipIndexer() = HipIndexer(nothing, nothing, nothing, nothing, nothing)
+
+# index!(indexer, A, maxindex) (src/utils.jl:306-314) on the device, stream-ordered.
+function index!(ix::HipIndexer, I::Union{HipVector{Int},HipMatrix{Int}}, maxindex)
+    pool = ndims(I) == 1 ? 1 : size(I, 1)
+    batch = size(I, ndims(I))
+    n = pool * batch
+    if ix.map === nothing || length(ix.map) < max(n, 1)
+        ix.cumulative_col = HipArray{Int64}(undef, n + 1)
+        ix.cumulative_off = HipArray{Int64}(undef, n + 1)
+        ix.map = HipArray{Int64}(undef, max(n, 1))
+        ix.nunique_dev = HipArray{Int64}(undef, 1)
+        nb = Ref{Int64}(0)
+        check(ccall((:et_index_workspace_size, libembtab), Cint, (Int64, Ref{Int64}), n, nb))
+        ix.workspace = HipArray{UInt8}(undef, nb[])
+    end
+    check(ccall((:et_index_build, libembtab), Cint,
+                (Ptr{Int64}, Int32, Int64, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Int64},
+                 Ptr{Int64}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                I.ptr, pool, pool, batch, maxindex, ix.cumulative_col.ptr, ix.cumulative_off.ptr,
+                ix.map.ptr, ix.nunique_dev.ptr, ix.workspace.ptr, length(ix.workspace), stream()))
+    return ix
+end
+nunique(ix::HipIndexer) = download(ix.nunique_dev)[1]
+
+# update!(table, grad, indexer, alpha, Val(NT)) (src/sparseupdate.jl:46-154) from a
+# device Indexer: every column serially in map order (et_update_indexed).
+function update!(table::HipTable{S,T}, grad::SparseEmbeddingUpdate, ix::HipIndexer, alpha,
+                 ::Val{Nontemporal} = Val(true)) where {S,T<:UpdateEltype,Nontemporal}
+    dp, dld = _ptr_ld(grad.delta)
+    tp, ldt, cpp = _device_table(table)
+    flags = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
+            (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED)
+    check(ccall((:et_update_indexed, libembtab), Cint,
+                (Cint, Ptr{Cvoid}, Int64, Int64, Int64, Int32, Ptr{Cvoid}, Int64, Ptr{Int64},
+                 Ptr{Int64}, Int64, Int64, Ptr{Int64}, Float64, UInt32, Ptr{Cvoid}),
+                et_dtype(T), tp, ldt, cpp, size(table, 2), size(table, 1), dp, dld,
+                ix.cumulative_col.ptr, ix.cumulative_off.ptr, 0, nunique(ix), ix.map.ptr,
+                Float64(alpha), flags, stream()))
     return nothing
 end
 
 # src/sparseupdate.jl:199-238: index all tables, telemetry_cb(), update all tables.
 # One device pipeline per (path, eltype) group, split at the same boundary
 # (ET_FLAG_SGD_INDEX_ONLY, then ET_FLAG_SGD_APPLY_ONLY from the same workspace);
-# telemetry_cb runs once the index phase is enqueued.  With fill_indexers (default),
-# indexers[i] receives table i's Indexer from the reference's own index! on a host copy
-# of the indices, on the CPU while the GPU runs the index phase.
+# telemetry_cb runs once the index phase is enqueued.  indexers[i] receives table i's
+# Indexer in the index phase as the reference's does: a HipIndexer is built on the device
+# (et_index_build, stream-ordered, no host work).  A host Indexer is filled by the
+# reference's own serial index! on a downloaded copy of the indices only when asked for
+# (fill_host_indexers = true): that costs a PCIe copy of every index array and a host
+# pass over every occurrence per step (272 MB and 34 M insertions at BASELINE config 4).
 const WORKSPACES = Dict{Int,Any}()
 function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  grads::AbstractVector{<:SparseEmbeddingUpdate},
                  indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
-                 telemetry_cb = Returns(nothing), fill_indexers::Bool = true,
-                 kw...) where {Nontemporal}
-    nt = Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)
+                 telemetry_cb = Returns(nothing), fill_host_indexers::Bool = false,
+                 exact::Bool = EXACT[], kw...) where {Nontemporal}
+    nt = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
+         (exact ? ET_FLAG_EXACT_UPDATE : UInt32(0))
     calls = []
     for fused in (true, false), T in (Float32, Float64, Float16)
         sel = [i for i in eachindex(tables) if _fused(tables[i]) == fused &&
@@ -383,8 +448,10 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                     length(ws), stream()))
     end
     run(ET_FLAG_SGD_INDEX_ONLY)
-    if fill_indexers
-        for i in eachindex(indexers, grads)
+    for i in eachindex(indexers, grads)
+        if indexers[i] isa HipIndexer
+            index!(indexers[i], grads[i].indices, size(tables[i], 2))
+        elseif fill_host_indexers
             EmbeddingTables.index!(indexers[i], download(grads[i].indices), size(tables[i], 2))
         end
     end
@@ -438,6 +505,15 @@ function comm_init(id::Vector{UInt8}, world, rank)
                 c, world, id, rank))
     return c[]
 end
+comm_destroy(comm::Ptr{Cvoid}) =
+    check(ccall((:et_comm_destroy, libembtab), Cint, (Ptr{Cvoid},), comm))
+# `world` simulated ranks of this process (one Julia task per rank, each on its own
+# stream): the world > 1 sharded step without `world` GPUs (et_comm_loopback).
+function comm_loopback(world)
+    cs = Vector{Ptr{Cvoid}}(undef, world)
+    check(ccall((:et_comm_loopback, libembtab), Cint, (Ptr{Ptr{Cvoid}}, Int32), cs, world))
+    return cs
+end
 
 mutable struct ShardedPreallocation
     handle::Ptr{Cvoid}
@@ -484,6 +560,7 @@ function maplookup!(S::ShardedPreallocation, dst::HipMatrix{T}, tables::Vector{<
 end
 
 export HipEmbedding, HipSplitEmbedding, HipArray, HipVector, HipMatrix, EmbtabError,
-    DeviceColumns, ShardedPreallocation, shard_plan, comm_id, comm_init
+    DeviceColumns, HipIndexer, ShardedPreallocation, shard_plan, comm_id, comm_init,
+    comm_destroy, comm_loopback
 
 end # module

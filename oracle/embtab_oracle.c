@@ -252,7 +252,7 @@ void orc_maplookup_prealloc(int dtype, const orc_lookup_desc* descs, int32_t nta
     c.batch = batch;
     c.dst = (char*)dst;
     c.ld_dst = ld_dst;
-    c.worksize = 1 + (batch - 1) / worksize_div; /* cdiv, src/lookup.jl:301-302 */
+    c.worksize = 1 + (batch - 1) / worksize_div; /* cdiv(a, b), src/lookup.jl:301-302 */
     c.len = (int64_t)worksize_div * ntables;
     c.f16_fp32_acc = f16_fp32_acc;
     atomic_init(&c.count, 1);
@@ -497,7 +497,7 @@ void orc_update_generic_f32(float* table, int64_t ld_table, int32_t dim, const f
             for (int32_t f = 0; f < dim; f++) scratch[f] += g[f];
         }
         float* w = table + (size_t)(k - 1) * ld_table;
-        /* f(x, y) = x - alpha * y  (src/sparseupdate.jl:78) */
+        /* f(x, y) = x - alpha * y  (src/sparseupdate.jl:88) */
         if (alpha_f64)
             for (int32_t f = 0; f < dim; f++)
                 w[f] = (float)((double)w[f] - alpha * (double)scratch[f]);
@@ -690,7 +690,7 @@ typedef struct {
 
 static void* multi_worker(void* arg) {
     multi_ctx* c = (multi_ctx*)arg;
-    /* Phase 1: index! every table (src/sparseupdate.jl:201-203) */
+    /* Phase 1: index! every table (src/sparseupdate.jl:210-213) */
     for (;;) {
         long t = atomic_fetch_add(&c->next_table, 1);
         if (t >= c->ntables) break;

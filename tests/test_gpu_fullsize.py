@@ -167,6 +167,55 @@ def test_config4_full_size(oracle, criteo):
     assert errs_chunked and max(errs_chunked) <= max(errs_serial)
 
 
+def test_config4_full_size_exact(oracle, criteo):
+    """north_star's parity bar for the fp32 update at full size: the exact mode
+    (ET_FLAG_EXACT_UPDATE: single-chunk columns in the chunk pass, every longer column a
+    serial chain) on the Zipf(1.05) batch of all 26 tables at B = 65536 is bit-identical
+    to the oracle's serial update (reference src/sparseupdate.jl:110-127) on sampled
+    columns of every table, always including each table's three hottest columns — the
+    hottest of the batch has 834,828 occurrences — and leaves untouched columns
+    bit-unchanged."""
+    tabs, _ = criteo
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(4000)
+    idx = [_zipf(R, (B, P), gen) for R in ROWS]
+    before = [A.data.clone() for A in tabs]
+    delta = torch.empty((B, D * len(ROWS)), dtype=torch.float32, device=DEV)
+    _lib.check(_lib.load().et_fill_uniform(_lib.ET_F32, delta.data_ptr(), delta.numel(), 4001, 0,
+                                           -1.0, 1.0, _lib.stream_handle()))
+    grads = [et.SparseEmbeddingUpdate(A.lookup_type, delta[:, t * D:(t + 1) * D], i)
+             for t, (A, i) in enumerate(zip(tabs, idx))]
+    et.update_(et.Descent(0.1), tabs, grads, [et.Indexer() for _ in tabs], exact=True)
+    torch.cuda.synchronize()
+    assert et.check_errors() == 0
+    g = torch.Generator().manual_seed(6)
+    hottest = 0
+    for t in range(len(ROWS)):
+        A, I, W0 = tabs[t], idx[t], before[t]
+        counts = torch.bincount(I.view(-1), minlength=ROWS[t] + 1)[1:]
+        touched = torch.nonzero(counts).view(-1)
+        mask = torch.ones(ROWS[t], dtype=torch.bool, device=DEV)
+        mask[touched] = False
+        assert torch.equal(A.data[mask], W0[mask])
+        pick = touched[torch.randperm(len(touched), generator=g)[:12].to(DEV)]
+        top = torch.topk(counts, min(3, ROWS[t])).indices
+        pick = torch.unique(torch.cat([pick, top]))
+        dl = grads[t].delta
+        for c in pick.tolist():
+            occ = torch.nonzero(I.view(-1) == c + 1).view(-1)     # occurrence order
+            n = len(occ)
+            if n == 0:
+                continue
+            hottest = max(hottest, n)
+            dsub = dl[occ // P].cpu().numpy()                       # one delta row per occurrence
+            w = W0[c:c + 1].cpu().numpy().copy()
+            oracle.sgd(w, dsub, np.ones(n, np.int64), 0.1, fused=True)
+            assert w[0].tobytes() == A.data[c].cpu().numpy().tobytes(), (t, c, n)
+            del dsub
+    assert hottest >= 800_000  # the serial chain of the hottest column was checked
+    del before
+
+
 def test_config1_reference_plumbing(oracle):
     """BASELINE config 1: SimpleEmbedding Float32 dim 16, 1000 columns, vector indices
     B = 128 — the GPU result equals the oracle's and the reference's naive lookup."""

@@ -595,6 +595,61 @@ def test_multi_table_update_phases_telemetry_and_indexers(oracle):
         assert np.array_equal(host(indexers[t].map), mp)
 
 
+def test_indexers_snapshot_the_indices_of_their_update(oracle):
+    """indexers[i] is table i's Indexer of the indices THAT update used
+    (src/sparseupdate.jl:211-213), even when the caller refills the index buffer in
+    place (the PreallocationPlan serving pattern) before reading it."""
+    rng = np.random.default_rng(211)
+    rows, B, P = [300, 77], 200, 9
+    hs = [rng.standard_normal((r, 64)).astype(np.float32) for r in rows]
+    tabs = [et.SimpleEmbedding(dev(h), et.Static(64)) for h in hs]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    idx = [dev(i) for i in hidx]
+    dd = dev(rng.standard_normal((B, 128)).astype(np.float32))
+    grads = [et.SparseEmbeddingUpdate(t.lookup_type, dd[:, 64 * k:64 * (k + 1)], i)
+             for k, (t, i) in enumerate(zip(tabs, idx))]
+    indexers = [et.Indexer(), et.Indexer()]
+    et.update_(et.Descent(0.1), tabs, grads, indexers)
+    for i, r in zip(idx, rows):  # refill in place before anyone reads the indexers
+        i.copy_(torch.from_numpy(rng.integers(1, r + 1, (B, P))))
+    for t in range(2):
+        cum, mp = oracle.index_build(hidx[t], rows[t])
+        assert np.array_equal(host(indexers[t].cumulative), cum)
+        assert np.array_equal(host(indexers[t].map), mp)
+
+
+def test_hot_pass_with_unaligned_preallocation_gradient(oracle):
+    """hot_pass=True on a Preallocation gradient whose row blocks are not 16-byte aligned
+    (prependrows k = 1): the host drops the hot-column pass for that group instead of
+    the update phase refusing the plan of the index phase; the result is the ordinary
+    update's (exact mode: the oracle's, bit for bit)."""
+    rng = np.random.default_rng(17)
+    rows, B, P, k = [400, 3000], 256, 20, 1
+    hs = [rng.standard_normal((r, 128)).astype(np.float32) for r in rows]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    hidx[0][:, :4] = 5  # a column of 1024 occurrences (a hot-pass candidate)
+    delta = rng.standard_normal((B, k + 256)).astype(np.float32)
+    dd = dev(delta)
+    for exact in (False, True):
+        tabs = [et.SimpleEmbedding(dev(h), et.Static(128)) for h in hs]
+        grads = [et.SparseEmbeddingUpdate(t.lookup_type, dd[:, k + 128 * j:k + 128 * (j + 1)],
+                                          dev(i)) for j, (t, i) in enumerate(zip(tabs, hidx))]
+        et.update_(et.Descent(0.1), tabs, grads, [et.Indexer(), et.Indexer()], exact=exact,
+                   hot_pass=True)
+        ref = [et.SimpleEmbedding(dev(h), et.Static(128)) for h in hs]
+        rgrads = [et.SparseEmbeddingUpdate(t.lookup_type, dd[:, k + 128 * j:k + 128 * (j + 1)],
+                                           dev(i)) for j, (t, i) in enumerate(zip(ref, hidx))]
+        et.update_(et.Descent(0.1), ref, rgrads, None, exact=exact)
+        for a, b in zip(tabs, ref):
+            assert torch.equal(a.data, b.data)
+        if exact:
+            for j in range(2):
+                w = hs[j].copy()
+                oracle.sgd(w, np.ascontiguousarray(delta[:, k + 128 * j:k + 128 * (j + 1)]),
+                           hidx[j], 0.1, fused=True)
+                assert bits_equal(host(tabs[j].data), w)
+
+
 def test_phased_hot_pass_null_delta_index_phase():
     """ET_FLAG_SGD_INDEX_ONLY with delta = NULL and the hot-column pass on: the index
     phase picks the hot columns from the tables alone, the update phase with an aligned
