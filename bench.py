@@ -411,6 +411,29 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
     upd_ms = _timed(upd, steps, warmup, stream)
     step_ms = _timed(step, steps, warmup, stream)
     overlap_ms = _timed(step_overlap, steps, warmup, stream)
+    # the other update mode, and how far the split mode lies from the exact (reference-
+    # order, src/sparseupdate.jl:110-127) result: both from the same tables, every element
+    other = not et.update.EXACT_DEFAULT
+    other_ms = _timed(lambda: et.update_(opt, tables, grads, indexers, exact=other), steps,
+                      warmup, stream)
+    w0 = [A.data.clone() for A in tables]
+    res = {}
+    for mode in (True, False):
+        et.update_(opt, tables, grads, None, exact=mode)
+        torch.cuda.synchronize()
+        res[mode] = [A.data.clone() for A in tables]
+        for A, w in zip(tables, w0):
+            A.data.copy_(w)
+    worst, over, differ = 0.0, 0, 0
+    for e, sp in zip(res[True], res[False]):
+        rel = (sp.double() - e.double()).abs() / e.double().abs().clamp_min(1e-30)
+        worst = max(worst, float(rel.max()))
+        over += int((rel > 1e-6).sum())
+        differ += int((sp != e).sum())
+    del res, w0
+    torch.cuda.empty_cache()
+    exact_ms = upd_ms if et.update.EXACT_DEFAULT else other_ms
+    split_ms = other_ms if et.update.EXACT_DEFAULT else upd_ms
     U = sum(int(torch.unique(i).numel()) for i in idx)
     occ = batch * POOL * len(tables)
     upd_bytes = occ * 8 + batch * len(tables) * DIM * 4 + 2 * U * DIM * 4
@@ -421,6 +444,13 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
             "step_note": "index phase of update! on a second stream beside the forward",
             "step_ms_serial": step_ms, "lookups_per_s_serial": occ / (step_ms * 1e-3),
             "forward_ms": fwd_ms, "update_ms": upd_ms,
+            "update_mode": "exact" if et.update.EXACT_DEFAULT else "split",
+            "update_exact_ms": exact_ms, "update_split_ms": split_ms,
+            "exact_over_split": exact_ms / split_ms,
+            # the split mode (long columns as ordered partial sums) against the exact one,
+            # over all 26 x 128 x R_t table elements after one update
+            "split_vs_exact_max_rel": worst, "split_elements_over_1e-6_rel": over,
+            "split_elements_differing": differ,
             "distinct_rows_U": U, "hottest_row_occurrences": hot,
             "update_algorithmic_bytes": upd_bytes,
             "update_achieved_GBs": upd_bytes / (upd_ms * 1e-3) / 1e9,

@@ -41,7 +41,7 @@ struct UpdatePack {
 };
 
 // Counters in the workspace.
-enum { kCntU = 0, kCntC = 1, kCntM = 2, kCntSlots = 16 };
+enum { kCntU = 0, kCntC = 1, kCntM = 2, kCntT = 3, kCntSlots = 16 };
 
 __device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, uint32_t key) {
     int t = 0;
@@ -1087,15 +1087,21 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
 // beyond the delta load; tools/gen_chain_asm.py).  Same additions in the same order as
 // the reference: bit-identical, and no partial sums to combine.
 //
-// Index phase: k_chain_count (run lengths -> S and the entry count per column),
-// k_chain_plan (entry offsets, columns ordered by cost so the longest chains are
-// dispatched first), k_chain_emit (the entries).  Update phase: the chain role of
+// Index phase, over tiles of kChainTile occurrences so a 834,828-occurrence column is
+// cut by ~200 workgroups rather than walked by one wave: k_chain_tiles (tiles per
+// column), k_chain_tcount (per tile, the entries its runs make at each S), k_chain_choose
+// (per column, S and the entry count), k_chain_plan (entry offsets, columns ordered by
+// cost so the longest chains are dispatched first), k_chain_emit (the entries).  Update phase: the chain role of
 // k_sgd_exact, beside the chunk pass (single-chunk columns) and the singles in ONE
 // launch, so the hottest chains (834,828 adds on the config-4 batch) overlap the rest.
-constexpr int kChainGroup = 24;  // entries per trip of the asm loop (3 batches of 8)
-constexpr int kChainPad = 16;    // readable entries past the last trip (its prefetches)
-constexpr int kChainEntryCost = 5;  // per-entry work besides the S fmas (gpr-idx, address,
-                                    // load, wait), in VALU issue slots
+constexpr int kChainGroup = kChainAsmTrip;  // entries per trip of the asm loop
+constexpr int kChainPad = kChainAsmPad;     // readable entries past the last trip
+constexpr int kChainEntryCost = kChainAsmEntryCost;  // issue slots per entry beside the fmas
+
+// A chain entry: r adds (r <= 16) of gradient column `bag` (< 2^24); 0 = padding.
+__device__ __forceinline__ uint32_t chain_entry(uint32_t r, uint32_t bag) {
+    return r << 24 | bag;
+}
 
 struct ChainCol {
     uint32_t key, e0, ngr, S;  // S == 0: no chain (out-of-range occurrences)
@@ -1119,97 +1125,66 @@ __device__ __forceinline__ uint32_t wave_excl_scan_u32(uint32_t v, int lane) {
     return x - v;
 }
 
-// Runs of equal bags in a column's sorted occurrences, one 64-occurrence slice at a
-// time.  Per lane: the run starting at this lane if it ends inside the slice.  Uniform:
-// the run carried in from earlier slices if it ends here.  The last run that starts in
-// the slice is carried out (open_start / open_bag, ~0u when there is none).
-struct SliceRuns {
-    bool lane_closed;
-    uint32_t lane_r, lane_bag;
-    bool open_closed;
-    uint32_t open_r, open_bag;
-};
+constexpr uint32_t kChainTile = 4096;  // occurrences per index-phase tile
+constexpr uint32_t kChainTileItems = 16;  // consecutive occurrences per thread in the
+                                           // entry scan (x 256)
 
-__device__ __forceinline__ SliceRuns slice_runs(const uint32_t* __restrict__ vals, uint32_t c0,
-                                                uint32_t se, uint32_t occ_off, uint32_t pool,
-                                                uint32_t& open_start, uint32_t& open_bag) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t pos = c0 + (uint32_t)lane;
-    const bool valid = pos < se;
-    const uint32_t bag = valid ? (vals[pos] - occ_off) / pool : 0xffffffffu;
-    const uint32_t prev = (uint32_t)__shfl_up((int)bag, 1, 64);
-    const bool head = valid && (lane == 0 ? (open_start == 0xffffffffu || bag != open_bag)
-                                          : bag != prev);
-    const uint64_t hm = (uint64_t)__ballot(head);
-    const uint64_t after = lane < 63 ? hm >> (lane + 1) : 0ull;
-    SliceRuns s;
-    s.lane_closed = head && after != 0ull;
-    s.lane_r = after ? (uint32_t)__ffsll((long long)after) : 0u;  // next head - this lane
-    s.lane_bag = bag;
-    s.open_closed = open_start != 0xffffffffu && hm != 0ull;
-    s.open_r = s.open_closed ? c0 + (uint32_t)(__ffsll((long long)hm) - 1) - open_start : 0u;
-    s.open_bag = open_bag;
-    if (hm != 0ull) {
-        const int last = 63 - __clzll((long long)hm);
-        open_start = c0 + (uint32_t)last;
-        open_bag = (uint32_t)__shfl((int)bag, last, 64);
+// A tile's bags in LDS: slot 0 the bag of the occurrence before the tile (~0 at the
+// column's start), slots 1..kChainTile the tile's, then kChainHalo past its end (~0 past
+// the column's end), so a run that starts in the tile is followed from LDS unless it is
+// longer than the halo.  Occurrences are sorted by position inside the column (stable
+// sort), and bag = (position - occ_off) / pool.
+constexpr uint32_t kChainHalo = 64;
+constexpr uint32_t kChainLds = kChainTile + 1 + kChainHalo;
+
+__device__ __forceinline__ void stage_bags(uint32_t* __restrict__ bags,
+                                           const uint32_t* __restrict__ vals, uint32_t ss,
+                                           uint32_t se, uint32_t a, uint32_t occ_off,
+                                           uint32_t pool) {
+    for (uint32_t i = threadIdx.x; i < kChainLds; i += blockDim.x) {
+        const uint32_t p = a - 1u + i;  // wraps to ~0 only when a == 0 (then p < ss fails)
+        bags[i] = (i > 0 || a > ss) && p < se ? (vals[p] - occ_off) / pool : 0xffffffffu;
     }
-    return s;
 }
 
-// Index phase 1: per chain column, S and the padded entry count.
-__global__ __launch_bounds__(256) void k_chain_count(UpdatePack pack, int ntables,
-                                                     const uint32_t* __restrict__ keys,
-                                                     const uint32_t* __restrict__ vals,
-                                                     const uint32_t* __restrict__ seg_start,
-                                                     const uint32_t* __restrict__ mlist,
-                                                     const uint32_t* __restrict__ counters,
-                                                     uint32_t sent, uint32_t* __restrict__ cnt,
-                                                     uint2* __restrict__ info) {
-    const uint32_t M = counters[kCntM];
-    const int lane = threadIdx.x & 63;
-    for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
-        const uint32_t u = mlist[m];
-        const uint32_t ss = seg_start[u], se = seg_start[u + 1], key = keys[ss];
-        if (key == sent) {
-            if (lane == 0) cnt[m] = 0, info[m] = make_uint2(0u, 0u);
-            continue;
-        }
-        const int t = table_of_key(pack, ntables, key);
-        const uint32_t occ_off = pack.occ_off[t], pool = (uint32_t)pack.d[t].pool;
-        uint32_t E[5] = {se - ss, 0u, 0u, 0u, 0u};  // entries at S = 1, 2, 4, 8, 16
-        uint32_t open_start = 0xffffffffu, open_bag = 0u;
-        for (uint32_t c0 = ss; c0 < se; c0 += 64) {
-            const SliceRuns sr = slice_runs(vals, c0, se, occ_off, pool, open_start, open_bag);
-            const uint32_t r = sr.lane_r;
-            // per-slice sums of ceil(r/S) over at most 64 occurrences fit 8 bits each
-            const uint32_t pk = sr.lane_closed ? (cdiv_u32(r, 2) | cdiv_u32(r, 4) << 8 |
-                                                  cdiv_u32(r, 8) << 16 | cdiv_u32(r, 16) << 24)
-                                               : 0u;
-            const uint32_t tot = wave_sum_u32(pk);
-#pragma unroll
-            for (int k = 1; k < 5; ++k) E[k] += (tot >> (8 * (k - 1))) & 0xffu;
-            if (sr.open_closed)
-#pragma unroll
-                for (int k = 1; k < 5; ++k) E[k] += cdiv_u32(sr.open_r, 1u << k);
-        }
-        {
-            const uint32_t r = se - open_start;  // the last run
-#pragma unroll
-            for (int k = 1; k < 5; ++k) E[k] += cdiv_u32(r, 1u << k);
-        }
-        int best = 0;
-        uint64_t bc = ~0ull;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const uint64_t c = (uint64_t)E[k] * (uint64_t)((1 << k) + kChainEntryCost);
-            if (c < bc) bc = c, best = k;
-        }
-        if (lane == 0) {
-            cnt[m] = cdiv_u32(E[best], kChainGroup) * kChainGroup + kChainPad;
-            info[m] = make_uint2(1u << best, E[best]);
-        }
-    }
+// Length of the run of equal bags starting at LDS slot i (a head, 1 <= i <= kChainTile),
+// followed into global memory past the halo.
+__device__ __forceinline__ uint32_t run_length(const uint32_t* __restrict__ bags, uint32_t i,
+                                               const uint32_t* __restrict__ vals, uint32_t se,
+                                               uint32_t a, uint32_t occ_off, uint32_t pool) {
+    const uint32_t b = bags[i];
+    uint32_t q = i + 1;
+    while (q < kChainLds && bags[q] == b) ++q;
+    if (q == kChainLds)
+        while (a - 1u + q < se && (vals[a - 1u + q] - occ_off) / pool == b) ++q;
+    return q - i;
+}
+
+// A tile's place: its column m, the column's occurrence range, the tile's first
+// occurrence and its index among the column's tiles.
+struct ChainTile {
+    uint32_t m, ss, se, a, ti, nt;
+    int t;  // table
+};
+
+__device__ __forceinline__ ChainTile chain_tile(const UpdatePack& pack, int ntables,
+                                                const uint32_t* __restrict__ keys,
+                                                const uint32_t* __restrict__ seg_start,
+                                                const uint32_t* __restrict__ mlist,
+                                                const uint32_t* __restrict__ tile0,
+                                                const uint32_t* __restrict__ tile_col,
+                                                uint32_t M, uint32_t T, uint32_t tile) {
+    ChainTile c;
+    c.m = tile_col[tile];
+    const uint32_t u = mlist[c.m];
+    c.ss = seg_start[u];
+    c.se = seg_start[u + 1];
+    const uint32_t t0 = tile0[c.m];
+    c.ti = tile - t0;
+    c.nt = (c.m + 1 < M ? tile0[c.m + 1] : T) - t0;
+    c.a = c.ss + c.ti * kChainTile;
+    c.t = table_of_key(pack, ntables, keys[c.ss]);
+    return c;
 }
 
 // Inclusive scan of one value per thread over a 1024-thread workgroup.
@@ -1233,7 +1208,122 @@ __device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32
     return v + off;
 }
 
-// Index phase 2 (one workgroup): entry offsets (exclusive scan of the padded counts) and
+// Index phase 1 (one workgroup): tiles per chain column (none for the out-of-range
+// sentinel column), the first tile of each column, the tile -> column map and the tile
+// total (counters[kCntT]).
+__global__ __launch_bounds__(1024) void k_chain_tiles(const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ seg_start,
+                                                      const uint32_t* __restrict__ mlist,
+                                                      uint32_t* __restrict__ counters,
+                                                      uint32_t sent, uint32_t* __restrict__ tile0,
+                                                      uint32_t* __restrict__ tile_col) {
+    __shared__ uint32_t lds16[16];
+    const uint32_t M = counters[kCntM];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < M; b0 += 1024) {
+        const uint32_t m = b0 + threadIdx.x;
+        uint32_t v = 0;
+        if (m < M) {
+            const uint32_t u = mlist[m], ss = seg_start[u], se = seg_start[u + 1];
+            v = keys[ss] == sent ? 0u : cdiv_u32(se - ss, kChainTile);
+        }
+        uint32_t total;
+        const uint32_t inc = block_inclusive_scan_1024(v, lds16, &total);
+        if (m < M) {
+            const uint32_t t0 = carry + inc - v;
+            tile0[m] = t0;
+            for (uint32_t k = 0; k < v; ++k) tile_col[t0 + k] = m;
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) counters[kCntT] = carry;
+}
+
+// Index phase 2: per tile, the entries its runs make at S = 1, 2, 4, 8, 16.
+__global__ __launch_bounds__(256) void k_chain_tcount(UpdatePack pack, int ntables,
+                                                      const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ vals,
+                                                      const uint32_t* __restrict__ seg_start,
+                                                      const uint32_t* __restrict__ mlist,
+                                                      const uint32_t* __restrict__ counters,
+                                                      const uint32_t* __restrict__ tile0,
+                                                      const uint32_t* __restrict__ tile_col,
+                                                      uint32_t* __restrict__ tcnt) {
+    __shared__ uint32_t bags[kChainLds];
+    __shared__ uint32_t red[4][5];
+    const uint32_t M = counters[kCntM], T = counters[kCntT];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+        const ChainTile c = chain_tile(pack, ntables, keys, seg_start, mlist, tile0, tile_col, M,
+                                       T, tile);
+        const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
+        const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
+        stage_bags(bags, vals, c.ss, c.se, c.a, occ_off, pool);
+        __syncthreads();
+        uint32_t E[5] = {0u, 0u, 0u, 0u, 0u};
+        for (uint32_t i = 1 + threadIdx.x; i <= n; i += 256) {
+            if (bags[i] == bags[i - 1]) continue;
+            const uint32_t r = run_length(bags, i, vals, c.se, c.a, occ_off, pool);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) E[k] += cdiv_u32(r, 1u << k);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t v = wave_sum_u32(E[k]);
+            if (lane == 0) red[wave][k] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < 5)
+            tcnt[5 * tile + threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                           red[2][threadIdx.x] + red[3][threadIdx.x];
+        __syncthreads();  // bags and red are reused by the next tile
+    }
+}
+
+// Index phase 3: per chain column (one wave), S minimising entries x (S + per-entry
+// overhead), and the padded entry count; (S, entries) in info.  A column without tiles
+// (the sentinel) gets S = 0: no chain.
+__global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ seg_start,
+                                                      const uint32_t* __restrict__ mlist,
+                                                      const uint32_t* __restrict__ counters,
+                                                      const uint32_t* __restrict__ tile0,
+                                                      const uint32_t* __restrict__ tcnt,
+                                                      uint32_t* __restrict__ cnt,
+                                                      uint2* __restrict__ info,
+                                                      ChainCol* __restrict__ chains) {
+    const uint32_t M = counters[kCntM], T = counters[kCntT];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
+        const uint32_t t0 = tile0[m], nt = (m + 1 < M ? tile0[m + 1] : T) - t0;
+        if (nt == 0) {
+            if (lane == 0) {
+                cnt[m] = 0u;
+                info[m] = make_uint2(0u, 0u);
+                chains[m] = ChainCol{keys[seg_start[mlist[m]]], 0u, 0u, 0u};
+            }
+            continue;
+        }
+        uint32_t E[5] = {0u, 0u, 0u, 0u, 0u};
+        for (uint32_t i = (uint32_t)lane; i < nt; i += 64)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) E[k] += tcnt[5 * (t0 + i) + k];
+        int best = 0;
+        uint64_t bc = ~0ull;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            E[k] = wave_sum_u32(E[k]);
+            const uint64_t c = (uint64_t)E[k] * (uint64_t)((1 << k) + kChainEntryCost);
+            if (c < bc) bc = c, best = k;
+        }
+        if (lane == 0) {
+            cnt[m] = cdiv_u32(E[best], kChainGroup) * kChainGroup + kChainPad;
+            info[m] = make_uint2(1u << best, E[best]);
+        }
+    }
+}
+
+// Index phase 4 (one workgroup): entry offsets (exclusive scan of the padded counts) and
 // the dispatch order: columns bucketed by log2 of their cost (entries x (S + overhead)),
 // costliest bucket first; the order inside a bucket is arbitrary (results never depend
 // on which wave takes a column).
@@ -1280,74 +1370,90 @@ __global__ __launch_bounds__(1024) void k_chain_plan(const uint32_t* __restrict_
 }
 
 // One run of r adds of delta column `bag` as ceil(r/S) entries (S adds each, the last
-// one the remainder): (delta element offset, S - adds).
-__device__ __forceinline__ void chain_put(uint2* __restrict__ ent, uint32_t at, uint32_t i,
-                                          uint32_t k, uint32_t r, uint32_t S, uint32_t off) {
+// one the remainder).
+__device__ __forceinline__ void chain_put(uint32_t* __restrict__ ent, uint32_t at, uint32_t i,
+                                          uint32_t k, uint32_t r, uint32_t S, uint32_t bag) {
     const uint32_t adds = i + 1 < k ? S : r - S * (k - 1);
-    ent[at] = make_uint2(off, S - adds);
+    ent[at] = chain_entry(adds, bag);
 }
 
-// Index phase 3: the entries, padded with (0, S) (masks all zero) to the planned count.
+// Index phase 5, per tile: the entries of the runs that start in it (after the entries
+// of the column's earlier tiles at the column's S, in occurrence order); the column's
+// last tile pads the entries with zeros (no adds) to the planned count and writes the
+// column's descriptor.  Runs are found on the LDS-staged bags (coalesced), their entry
+// offsets by a block scan over 16 consecutive occurrences per thread.
 __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables,
                                                     const uint32_t* __restrict__ keys,
                                                     const uint32_t* __restrict__ vals,
                                                     const uint32_t* __restrict__ seg_start,
                                                     const uint32_t* __restrict__ mlist,
                                                     const uint32_t* __restrict__ counters,
+                                                    const uint32_t* __restrict__ tile0,
+                                                    const uint32_t* __restrict__ tile_col,
+                                                    const uint32_t* __restrict__ tcnt,
                                                     const uint32_t* __restrict__ cnt,
                                                     const uint2* __restrict__ info,
                                                     const uint32_t* __restrict__ e0s,
-                                                    uint2* __restrict__ ent,
+                                                    uint32_t* __restrict__ ent,
                                                     ChainCol* __restrict__ chains) {
-    const uint32_t M = counters[kCntM];
-    const int lane = threadIdx.x & 63;
-    for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
-        const uint32_t P = cnt[m];
-        const uint32_t u = mlist[m];
-        const uint32_t ss = seg_start[u], se = seg_start[u + 1], key = keys[ss];
-        if (P == 0) {
-            if (lane == 0) chains[m] = ChainCol{key, 0u, 0u, 0u};
-            continue;
-        }
-        const uint32_t S = info[m].x, e0 = e0s[m];
-        const int t = table_of_key(pack, ntables, key);
-        const uint32_t occ_off = pack.occ_off[t], pool = (uint32_t)pack.d[t].pool;
-        const uint32_t ld = (uint32_t)pack.d[t].ld_delta;
-        uint32_t at = e0;
-        uint32_t open_start = 0xffffffffu, open_bag = 0u;
-        for (uint32_t c0 = ss; c0 < se; c0 += 64) {
-            const SliceRuns sr = slice_runs(vals, c0, se, occ_off, pool, open_start, open_bag);
-            if (sr.open_closed) {  // the carried run precedes this slice's runs
-                const uint32_t k = cdiv_u32(sr.open_r, S);
-                for (uint32_t i = lane; i < k; i += 64)
-                    chain_put(ent, at + i, i, k, sr.open_r, S, sr.open_bag * ld);
-                at += k;
-            }
-            const uint32_t k = sr.lane_closed ? cdiv_u32(sr.lane_r, S) : 0u;
-            const uint32_t pre = wave_excl_scan_u32(k, lane);
-            for (uint32_t i = 0; i < k; ++i)
-                chain_put(ent, at + pre + i, i, k, sr.lane_r, S, sr.lane_bag * ld);
-            at += (uint32_t)__shfl((int)(pre + k), 63, 64);
-        }
-        {
-            const uint32_t r = se - open_start, k = cdiv_u32(r, S);
-            for (uint32_t i = lane; i < k; i += 64) chain_put(ent, at + i, i, k, r, S, open_bag * ld);
+    __shared__ uint32_t bags[kChainLds];
+    __shared__ uint32_t rl[kChainTile];  // run length at a head, 0 elsewhere
+    __shared__ uint32_t red[2][4];
+    const uint32_t M = counters[kCntM], T = counters[kCntT];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+        const ChainTile c = chain_tile(pack, ntables, keys, seg_start, mlist, tile0, tile_col, M,
+                                       T, tile);
+        const uint2 in = info[c.m];
+        const uint32_t S = in.x, kS = (uint32_t)(__ffs((int)S) - 1);
+        const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
+        const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
+        stage_bags(bags, vals, c.ss, c.se, c.a, occ_off, pool);
+        __syncthreads();
+        for (uint32_t i = 1 + threadIdx.x; i <= kChainTile; i += 256)
+            rl[i - 1] = i <= n && bags[i] != bags[i - 1]
+                            ? run_length(bags, i, vals, c.se, c.a, occ_off, pool) : 0u;
+        // entries of the column's earlier tiles, and of this thread's 16 occurrences
+        uint32_t before = 0, mine = 0;
+        const uint32_t t0 = tile - c.ti;
+        for (uint32_t i = threadIdx.x; i < c.ti; i += 256) before += tcnt[5 * (t0 + i) + kS];
+        __syncthreads();
+        const uint32_t j0 = threadIdx.x * kChainTileItems;
+#pragma unroll
+        for (uint32_t j = 0; j < kChainTileItems; ++j) mine += cdiv_u32(rl[j0 + j], S);
+        before = wave_sum_u32(before);
+        const uint32_t pre = wave_excl_scan_u32(mine, lane);
+        if (lane == 63) red[0][wave] = pre + mine;
+        if (lane == 0) red[1][wave] = before;
+        __syncthreads();
+        uint32_t at = e0s[c.m] + red[1][0] + red[1][1] + red[1][2] + red[1][3] + pre;
+        for (int w = 0; w < wave; ++w) at += red[0][w];
+        for (uint32_t j = 0; j < kChainTileItems; ++j) {
+            const uint32_t r = rl[j0 + j];
+            if (r == 0u) continue;
+            const uint32_t k = cdiv_u32(r, S), bag = bags[j0 + j + 1];
+            for (uint32_t i = 0; i < k; ++i) chain_put(ent, at + i, i, k, r, S, bag);
             at += k;
         }
-        for (uint32_t i = at + lane; i < e0 + P; i += 64) ent[i] = make_uint2(0u, S);
-        if (lane == 0) chains[m] = ChainCol{key, e0, (P - kChainPad) / kChainGroup, S};
+        if (c.ti + 1 == c.nt) {
+            const uint32_t e0 = e0s[c.m], P = cnt[c.m];
+            for (uint32_t i = e0 + in.y + threadIdx.x; i < e0 + P; i += 256) ent[i] = 0u;
+            if (threadIdx.x == 0)
+                chains[c.m] = ChainCol{keys[c.ss], e0, (P - kChainPad) / kChainGroup, S};
+        }
+        __syncthreads();  // bags, rl and red are reused by the next tile
     }
 }
 
 // Debug check of the chain plan (ET_CHAIN_CHECK=1): every entry of every chain addresses
-// a gradient column of its table's batch with a mask index <= S, the entries carrying
+// a gradient column of its table's batch with at most S adds, the entries carrying
 // adds number exactly E and precede the padding; a violation is counted in the device
-// error word (et_check_errors) as 1 << 20 and the entry neutralised to (0, S).
+// error word (et_check_errors) as 1 << 20 and the entry neutralised to 0.
 __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntables,
                                                      const uint32_t* __restrict__ counters,
                                                      const uint32_t* __restrict__ cnt,
                                                      const uint2* __restrict__ info,
-                                                     uint2* __restrict__ ent,
+                                                     uint32_t* __restrict__ ent,
                                                      const ChainCol* __restrict__ chains,
                                                      const uint32_t* __restrict__ order) {
     const uint32_t M = counters[kCntM];
@@ -1359,16 +1465,16 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
         const uint32_t P = cnt[m];
         if (c.S == 0u) continue;
         const int t = table_of_key(pack, ntables, c.key);
-        const uint64_t lim = (uint64_t)pack.d[t].batch * (uint64_t)pack.d[t].ld_delta;
+        const uint64_t lim = (uint64_t)pack.d[t].batch;
         uint32_t bad = 0, real = 0, pad_then_real = 0;
         if (P != c.ngr * kChainGroup + kChainPad || c.S != info[m].x) bad = 1;
         for (uint32_t i = lane; i < P; i += 64) {
-            const uint2 e = ent[c.e0 + i];
-            const bool ok = (uint64_t)e.x < lim && e.y <= c.S;
-            if (!ok) ent[c.e0 + i] = make_uint2(0u, c.S);
+            const uint32_t e = ent[c.e0 + i], r = e >> 24;
+            const bool ok = (uint64_t)(e & 0xffffffu) < lim && r <= c.S;
+            if (!ok) ent[c.e0 + i] = 0u;
             bad += ok ? 0u : 1u;
-            real += (ok && e.y < c.S) ? 1u : 0u;
-            pad_then_real += (ok && e.y < c.S && i >= info[m].y) ? 1u : 0u;
+            real += (ok && r > 0u) ? 1u : 0u;
+            pad_then_real += (ok && r > 0u && i >= info[m].y) ? 1u : 0u;
         }
         bad = wave_sum_u32(bad) + wave_sum_u32(pad_then_real);
         real = wave_sum_u32(real);
@@ -1383,7 +1489,7 @@ __device__ __forceinline__ void sgd_chain_body(const UpdatePack& pack, int ntabl
                                                const uint32_t* __restrict__ counters,
                                                const ChainCol* __restrict__ chains,
                                                const uint32_t* __restrict__ order,
-                                               const uint2* __restrict__ ent, int ns,
+                                               const uint32_t* __restrict__ ent, int ns,
                                                float eta32, double eta64, uint32_t bid,
                                                uint32_t nblk, bool plain) {
     const int lane = threadIdx.x & 63;
@@ -1392,6 +1498,10 @@ __device__ __forceinline__ void sgd_chain_body(const UpdatePack& pack, int ntabl
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t M = counters[kCntM];
     const uint32_t nw = nblk * 4u, items = M * (uint32_t)ns;
+    // A chain issues a dependent VALU op about every 4.4 cycles, i.e. it alone nearly fills
+    // its SIMD's VALU: top priority, so the co-resident chunk-pass and singles waves (memory
+    // bound) take the leftover issue slots instead of stretching the critical chain.
+    __builtin_amdgcn_s_setprio(3);
     for (uint32_t it = bid * 4u + (uint32_t)wave; it < items; it += nw) {
         const ChainCol c = chains[order[it / (uint32_t)ns]];
         if (c.S == 0u) continue;
@@ -1399,29 +1509,36 @@ __device__ __forceinline__ void sgd_chain_body(const UpdatePack& pack, int ntabl
         const et_update_desc& d = pack.d[t];
         const int f = (int)(it % (uint32_t)ns) * 64 + lane;
         if ((int)(it % (uint32_t)ns) * 64 >= d.dim) continue;  // uniform
-        const float* xb = reinterpret_cast<const float*>(d.delta) + (f < d.dim ? f : d.dim - 1);
-        const uint32_t* e = reinterpret_cast<const uint32_t*>(ent + c.e0);
+        const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
+        const uint32_t ld = (uint32_t)d.ld_delta;
+        // the gradient base as a wave-uniform (SGPR) pointer
+        const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
+        const float* delta = reinterpret_cast<const float*>(
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
+        const uint32_t* e = ent + c.e0;
         float acc = 0.0f;
         if (plain) {  // debug reference of the asm loop: the same adds, plainly
             const uint32_t ne = c.ngr * kChainGroup;
             for (uint32_t h = 0; h < ne; ++h) {
-                const uint2 en = ent[c.e0 + h];
-                const float x = xb[en.x];
-                for (uint32_t k = en.y; k < c.S; ++k) acc = acc + x;
+                const uint32_t en = e[h];
+                const float x = delta[(uint64_t)(en & 0xffffffu) * ld + fc];
+                for (uint32_t k = 0; k < (en >> 24); ++k) acc = acc + x;
             }
         } else
         switch (c.S) {
-            case 1: acc = chain_walk_asm<1>(e, c.ngr, xb, 0.0f); break;
-            case 2: acc = chain_walk_asm<2>(e, c.ngr, xb, 0.0f); break;
-            case 4: acc = chain_walk_asm<4>(e, c.ngr, xb, 0.0f); break;
-            case 8: acc = chain_walk_asm<8>(e, c.ngr, xb, 0.0f); break;
-            default: acc = chain_walk_asm<16>(e, c.ngr, xb, 0.0f); break;
+            case 1: acc = chain_walk_asm<1>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+            case 2: acc = chain_walk_asm<2>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+            case 4: acc = chain_walk_asm<4>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+            case 8: acc = chain_walk_asm<8>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+            default: acc = chain_walk_asm<16>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
         }
         if (f < d.dim) {
             float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
             store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
         }
     }
+    __builtin_amdgcn_s_setprio(0);
 }
 
 // The whole update phase of an exact Float32 call in one launch: blocks [0, ncb) the
@@ -1433,7 +1550,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, uint32_t sent, float eta32, double eta64,
     uint32_t my_mask, const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint2* __restrict__ ent, int ns, uint32_t ncb, uint32_t nch, int plain) {
+    const uint32_t* __restrict__ ent, int ns, uint32_t ncb, uint32_t nch, int plain) {
     if (blockIdx.x < ncb) {
         sgd_chain_body<MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta32, eta64,
                                  blockIdx.x, ncb, plain != 0);
@@ -1541,14 +1658,23 @@ struct UpdateWs {
     // exact Float32 mode: chain entries (aliasing `partials`: that mode has no partial
     // sums), per chain column (multi-chunk list slot) its descriptor, padded entry count,
     // (S, entries), entry offset, and the cost-ordered slot list
-    uint2* chain_ent;
+    uint32_t* chain_ent;
     ChainCol* chains;
     uint32_t *chain_cnt, *chain_e0, *chain_order;
     uint2* chain_info;
+    // the index phase's tiles: first tile per column, tile -> column, entries per tile at
+    // S = 1..16
+    uint32_t *chain_tile0, *chain_tile_col, *chain_tcnt;
     int64_t bytes;
 };
 
 inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+// Index-phase tiles of the chain columns: at most one partial tile per column plus the
+// full ones.
+inline int64_t chain_tiles_max(int64_t n, uint32_t chunk) {
+    return n / kChainTile + n / chunk + 3;
+}
 
 // Lay out (or size, when base == nullptr) the update workspace for n occurrences and
 // partial rows of pdim floats.
@@ -1585,14 +1711,18 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
     // 8 bytes per partial element: float (vector path / fp32 accumulators) or double; the
     // exact mode's chain entries (8 bytes, at most one per occurrence + padding) alias it
     const int64_t part_b = 8 * max_partials * (int64_t)(pdim > 0 ? pdim : 1);
-    const int64_t chain_b = 8 * (n + (int64_t)(kChainGroup + kChainPad) * mmax + 64);
+    const int64_t chain_b = 4 * (n + (int64_t)(kChainGroup + kChainPad) * mmax + 64);
     w.partials = (float*)take(part_b > chain_b ? part_b : chain_b);
-    w.chain_ent = (uint2*)w.partials;
+    w.chain_ent = (uint32_t*)w.partials;
     w.chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * mmax);
     w.chain_cnt = (uint32_t*)take(4 * mmax);
     w.chain_e0 = (uint32_t*)take(4 * mmax);
     w.chain_order = (uint32_t*)take(4 * mmax);
     w.chain_info = (uint2*)take(8 * mmax);
+    const int64_t tmax = chain_tiles_max(n, chunk);
+    w.chain_tile0 = (uint32_t*)take(4 * mmax);
+    w.chain_tile_col = (uint32_t*)take(4 * tmax);
+    w.chain_tcnt = (uint32_t*)take(20 * tmax);
     w.hot_nw = (int)((hot_batch + kHotWin - 1) / kHotWin);
     w.hot_hist = nullptr;
     w.hot_cnt = nullptr;
@@ -1700,14 +1830,22 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     if (chain) {  // exact Float32 mode: the multi-chunk columns become serial chains
         const int64_t mmax = n / chunk + 2;
         const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
-        hipLaunchKernelGGL(k_chain_count, dim3(cg), dim3(256), 0, s, pack, ntables, out.keys,
-                           out.vals, w.seg_start, w.mlist, w.counters, sent, w.chain_cnt,
-                           w.chain_info);
+        const int64_t tmax = chain_tiles_max(n, chunk);
+        const unsigned tg = (unsigned)(tmax < 8192 ? tmax : 8192);
+        hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, out.keys, w.seg_start,
+                           w.mlist, w.counters, sent, w.chain_tile0, w.chain_tile_col);
+        hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                           w.chain_tile_col, w.chain_tcnt);
+        hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
+                           w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
+                           w.chain_info, w.chains);
         hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
                            w.chain_info, w.chain_e0, w.chain_order);
-        hipLaunchKernelGGL(k_chain_emit, dim3(cg), dim3(256), 0, s, pack, ntables, out.keys,
-                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_cnt, w.chain_info,
-                           w.chain_e0, w.chain_ent, w.chains);
+        hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                           w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
+                           w.chain_ent, w.chains);
         ET_LAUNCH_CHECK("k_chain_emit");
         static const bool check = [] {
             const char* e = getenv("ET_CHAIN_CHECK");
@@ -1773,11 +1911,12 @@ inline bool sgd_chunks_occ5() {
 }
 
 // Workgroups of the exact mode's chain role: one item per (chain column, 64-feature slice),
-// cost-ordered; 512 workgroups (2048 waves) cover the ~17 K items of the config-4 batch in
-// about eight rounds, the first round holding the longest chains.
+// cost-ordered; at most 256 workgroups (1024 waves: one per SIMD when spread one per CU)
+// so no two of the first round's chains, the longest, share a SIMD's VALU; the ~17 K
+// items of the config-4 batch take about 17 rounds, the later ones short.
 inline unsigned chain_blocks(int64_t n) {
     const int64_t g = cdiv64(n, 65536);
-    return (unsigned)(g < 1 ? 1 : g > 512 ? 512 : g);
+    return (unsigned)(g < 1 ? 1 : g > 256 ? 256 : g);
 }
 
 // The update phase of an exact Float32 call: chains + chunk pass + singles in one launch
@@ -2043,11 +2182,14 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool exact = (flags & ET_FLAG_EXACT_UPDATE) != 0;
     // Exact Float32: columns longer than a chunk are summed as serial chains (k_chain_*,
-    // k_sgd_exact), which address a gradient column by a 32-bit element offset.  Other
-    // exact calls keep every column in one chunk (a chunk spans a whole segment).
+    // k_sgd_exact), whose entries hold a 24-bit bag and whose loop addresses the gradient
+    // by a 32-bit byte offset (bag * ld * 4 from 24-bit factors).  Other exact calls keep
+    // every column in one chunk (a chunk spans a whole segment).
     bool chain = exact && dtype == ET_F32;
     for (int t = 0; t < ntables && chain; ++t)
-        if ((uint64_t)descs[t].batch * (uint64_t)descs[t].ld_delta >= 0xffffffffull) chain = false;
+        if (descs[t].batch >= (1 << 24) || descs[t].ld_delta >= (1 << 22) ||
+            (uint64_t)descs[t].batch * (uint64_t)descs[t].ld_delta >= (1ull << 30))
+            chain = false;
     const uint32_t chunk =
         exact && !chain ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff) : et::kChunk;
     int nhot;

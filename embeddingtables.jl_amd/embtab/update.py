@@ -309,7 +309,13 @@ def _sparse_sgd(descs, eta: float, flags: int, device, dtype=torch.float32):
                                flags, ws.data_ptr(), ws.numel(), _lib.stream_handle(device)))
 
 
-def update_(*args, nontemporal: bool | None = None, exact: bool = False,
+# The exact update (ET_FLAG_EXACT_UPDATE: every column's gradient summed serially in the
+# reference's order, src/sparseupdate.jl:110-127 — bit-identical) is the default; exact=False
+# selects the split mode (columns longer than ET_SGD_CHUNK summed as ordered partial sums).
+EXACT_DEFAULT = True
+
+
+def update_(*args, nontemporal: bool | None = None, exact: bool | None = None,
             f16_fp32_acc: bool = False, hot_pass: bool = False, **kw):
     """Julia's ``update!`` (multiple dispatch on the argument types):
 
@@ -320,13 +326,16 @@ def update_(*args, nontemporal: bool | None = None, exact: bool = False,
     * ``update_(table, grad, indexer_or_view, alpha, [nontemporal])`` — update from a
       prebuilt Indexer / IndexerView range (:46-154).
 
-    ``exact=True`` sums every column's gradient serially (bit-identical to the
-    reference even for hot columns); the default splits occurrence lists longer than
+    ``exact`` (default EXACT_DEFAULT = True) sums every column's gradient serially
+    (bit-identical to the reference even for hot columns: longer columns run as serial
+    chains beside the chunk pass); ``exact=False`` splits occurrence lists longer than
     ET_SGD_CHUNK (256) into partial sums combined in a fixed order (deterministic).  Float16 tables
     use Julia's Float16 arithmetic unless ``f16_fp32_acc`` (sums in Float32).
     ``hot_pass=True`` (experimental, ET_FLAG_SGD_HOT_PASS) sums the longest occurrence
     lists of Float32 dim-128 tables bag-major (deterministic, not bit-identical to the
     default split)."""
+    if exact is None:
+        exact = EXACT_DEFAULT
     if args and isinstance(args[0], Descent):
         opt = args[0]
         if isinstance(args[1], AbstractEmbeddingTable):
@@ -453,8 +462,10 @@ class PhasedUpdate:
     before ``update_``.  Results are bit-identical to ``update_(opt, tables, grads,
     indexers)`` with the same ``exact`` / ``nontemporal`` / ``f16_fp32_acc``."""
 
-    def __init__(self, tables, grads, *, nontemporal: bool = True, exact: bool = False,
+    def __init__(self, tables, grads, *, nontemporal: bool = True, exact: bool | None = None,
                  f16_fp32_acc: bool = False, hot_pass: bool = False):
+        if exact is None:
+            exact = EXACT_DEFAULT
         tables, grads = list(tables), list(grads)
         if len(tables) != len(grads):
             raise ArgumentError("tables and grads differ in length")

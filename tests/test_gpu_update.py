@@ -92,7 +92,7 @@ def test_update_exact_vs_oracle(oracle, dim, static, reducing):
 
 def test_update_hot_rows_chunked_vs_exact(oracle):
     """Zipf-skewed indices.  Exact mode: bit-identical to the reference's serial sum
-    (north_star's 1e-6-relative bound, met with zero error).  Default mode: columns with
+    (north_star's 1e-6-relative bound, met with zero error).  Split mode: columns with
     at most ET_SGD_CHUNK occurrences are bit-identical too; longer occurrence lists are
     summed as ordered partial sums (deterministic), whose error is bounded by 1e-6 of the
     summation-error scale |w| + eta * sum|delta| of the exact (fp64) update and is no
@@ -140,7 +140,8 @@ def test_update_hot_rows_chunked_vs_exact(oracle):
     assert big.any() and rel_chunked.max() <= rel_serial.max()
     # deterministic: the chunked result repeats exactly
     A = et.SimpleEmbedding(dev(base), et.Static(dim))
-    et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), dev(I)))
+    et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), dev(I)),
+               exact=False)
     assert bits_equal(host(A.data), res[False])
 
 

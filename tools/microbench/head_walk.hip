@@ -230,24 +230,25 @@ __global__ void k_chain(const uint2* __restrict__ ent, int ne, const float* __re
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
-// the generated hand-scheduled loop (csrc/et_chain_asm.h): entries (bag * ld, S - r)
+// the generated hand-scheduled loop (csrc/et_chain_asm.h): entries r << 24 | bag
 template <int S>
-__global__ void k_chain_asm(const uint32_t* __restrict__ ent, int ngr, const float* __restrict__ delta,
-                            float* out, long long* cyc) {
+__global__ void k_chain_asm(const uint32_t* __restrict__ ent, int trips, const float* __restrict__ delta,
+                            int ld, float* out, long long* cyc) {
     const long long t0 = __builtin_amdgcn_s_memtime();
-    const float acc = et::chain_walk_asm<S>(ent, (uint32_t)ngr, delta + threadIdx.x, 0.0f);
+    const float acc = et::chain_walk_asm<S>(ent, (uint32_t)trips, delta, 4u * threadIdx.x,
+                                            4u * (uint32_t)ld, 0.0f);
     const long long t1 = __builtin_amdgcn_s_memtime();
     out[threadIdx.x] = acc;
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
 // reference: the same entries summed with plain sequential adds
-__global__ void k_chain_ref(const uint32_t* __restrict__ ent, int ne, int S,
+__global__ void k_chain_ref(const uint32_t* __restrict__ ent, int ne, int ld,
                             const float* __restrict__ delta, float* out) {
     float acc = 0.0f;
     for (int h = 0; h < ne; ++h) {
-        const float x = delta[ent[2 * h] + threadIdx.x];
-        const int r = S - (int)ent[2 * h + 1];
+        const float x = delta[(size_t)(ent[h] & 0xffffffu) * ld + threadIdx.x];
+        const int r = (int)(ent[h] >> 24);
         for (int k = 0; k < r; ++k) acc = acc + x;
     }
     out[threadIdx.x] = acc;
@@ -347,31 +348,39 @@ int main() {
             printf("    %.1f cycles per entry\n", (double)best / ne);
             CHECK(hipFree(dent));
 
-            {  // the hand-scheduled loop on the same run lengths
+            // the hand-scheduled loop on the same run lengths: gradient in L2 (the
+            // columns above) and in HBM (65,536 columns of the config-4 stride, 872 MB)
+            for (int big = 0; big < 2; ++big) {
+                const int bcols = big ? 65536 : ncols, bld = big ? 3328 : ld;
+                float* bdelta = delta;
+                if (big) {
+                    CHECK(hipMalloc(&bdelta, (size_t)bcols * bld * 4));
+                    std::vector<float> hb((size_t)bcols * bld);
+                    for (size_t i = 0; i < hb.size(); ++i)
+                        hb[i] = 1e-3f * (float)((i * 7919) % 1000) - 0.5f;
+                    CHECK(hipMemcpy(bdelta, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+                }
                 std::vector<uint32_t> ea;
                 for (size_t i = 0; i < (size_t)ne; ++i) {
-                    ea.push_back(ee[2 * i] * (uint32_t)ld);
-                    ea.push_back((uint32_t)S - ee[2 * i + 1] / 64u);
+                    const uint32_t bag = big ? (uint32_t)(rand() % bcols) : ee[2 * i];
+                    ea.push_back((ee[2 * i + 1] / 64u) << 24 | bag);
                 }
-                const int ngr = (ne + 23) / 24;
-                while (ea.size() < (size_t)(ngr * 24 + 16) * 2) {
-                    ea.push_back(0u);
-                    ea.push_back((uint32_t)S);
-                }
+                const int trips = (ne + 63) / 64;
+                ea.resize((size_t)(trips * 64 + 64), 0u);
                 uint32_t* da;
                 float* ref;
                 CHECK(hipMalloc(&da, ea.size() * 4));
                 CHECK(hipMalloc(&ref, 64 * 4));
                 CHECK(hipMemcpy(da, ea.data(), ea.size() * 4, hipMemcpyHostToDevice));
-                snprintf(name, sizeof name, "asm chain S=%d", S);
+                snprintf(name, sizeof name, "asm chain S=%d (%s)", S, big ? "HBM" : "L2");
                 if (S == 16)
-                    run(name, [&] { k_chain_asm<16><<<1, 64>>>(da, ngr, delta, out, cyc); }, (double)adds2);
+                    run(name, [&] { k_chain_asm<16><<<1, 64>>>(da, trips, bdelta, bld, out, cyc); }, (double)adds2);
                 else
-                    run(name, [&] { k_chain_asm<4><<<1, 64>>>(da, ngr, delta, out, cyc); }, (double)adds2);
+                    run(name, [&] { k_chain_asm<4><<<1, 64>>>(da, trips, bdelta, bld, out, cyc); }, (double)adds2);
                 long long best2 = 0;
                 CHECK(hipMemcpy(&best2, cyc, 8, hipMemcpyDeviceToHost));
                 printf("    %.1f cycles per entry\n", (double)best2 / ne);
-                k_chain_ref<<<1, 64>>>(da, ne, S, delta, ref);
+                k_chain_ref<<<1, 64>>>(da, ne, bld, bdelta, ref);
                 CHECK(hipDeviceSynchronize());
                 float a[64], b[64];
                 CHECK(hipMemcpy(a, out, 256, hipMemcpyDeviceToHost));
@@ -381,6 +390,7 @@ int main() {
                 printf("    bit-identical to sequential adds: %s (%d lanes differ)\n", bad ? "NO" : "yes", bad);
                 CHECK(hipFree(da));
                 CHECK(hipFree(ref));
+                if (big) CHECK(hipFree(bdelta));
             }
         }
     }
