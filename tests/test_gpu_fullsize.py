@@ -111,9 +111,11 @@ def _zipf(R, shape, gen):
 
 
 def test_config4_full_size(oracle, criteo):
-    """Zipf(1.05) forward + fused Descent(0.1) on all 26 tables at B = 65536; every
-    table is checked: untouched columns unchanged, 24 sampled touched columns plus the
-    hottest against the oracle's serial update."""
+    """Zipf(1.05) forward + fused Descent(0.1) on all 26 tables at B = 65536 in the
+    split mode (exact=False: columns longer than one chunk summed as ordered partials);
+    every table is checked: untouched columns unchanged, 24 sampled touched columns plus
+    the hottest against the oracle's serial update (bit-identical up to one chunk, within
+    the summation bound beyond).  The default (exact) mode is the next test."""
     tabs, _ = criteo
     gen = torch.Generator(device=DEV)
     gen.manual_seed(4000)
@@ -124,7 +126,7 @@ def test_config4_full_size(oracle, criteo):
     _lib.check(_lib.load().et_fill_uniform(_lib.ET_F32, delta.data_ptr(), delta.numel(), 4001, 0,
                                            -1.0, 1.0, _lib.stream_handle()))
     grads = back(delta)[2]
-    et.update_(et.Descent(0.1), tabs, grads, [et.Indexer() for _ in tabs])
+    et.update_(et.Descent(0.1), tabs, grads, [et.Indexer() for _ in tabs], exact=False)
     torch.cuda.synchronize()
     assert et.check_errors() == 0
     g = torch.Generator().manual_seed(5)
