@@ -25,6 +25,8 @@
 // or  w = w - eta*acc  (unfused, the generic path; optionally evaluated in Float64 as
 // the reference's multi-table generic path does), chosen by ET_FLAG_SGD_UNFUSED /
 // ET_FLAG_SGD_F64_ALPHA.
+#include <mutex>
+
 #include "et_common.h"
 #include "et_chain_asm.h"
 #include "et_sort.hip"
@@ -1209,9 +1211,12 @@ __device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32
 }
 
 // Index phase 1 (one workgroup): tiles per chain column (none for the out-of-range
-// sentinel column), the first tile of each column, the tile -> column map and the tile
-// total (counters[kCntT]).
-__global__ __launch_bounds__(1024) void k_chain_tiles(const uint32_t* __restrict__ keys,
+// sentinel column, nor for the columns of early-chain tables, ec_mask: those chains are
+// planned from the index arrays, k_ec_*), the first tile of each column, the tile ->
+// column map and the tile total (counters[kCntT]).
+__global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntables,
+                                                      uint32_t ec_mask,
+                                                      const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ seg_start,
                                                       const uint32_t* __restrict__ mlist,
                                                       uint32_t* __restrict__ counters,
@@ -1225,7 +1230,9 @@ __global__ __launch_bounds__(1024) void k_chain_tiles(const uint32_t* __restrict
         uint32_t v = 0;
         if (m < M) {
             const uint32_t u = mlist[m], ss = seg_start[u], se = seg_start[u + 1];
-            v = keys[ss] == sent ? 0u : cdiv_u32(se - ss, kChainTile);
+            const uint32_t k0 = keys[ss];
+            v = k0 == sent || ((ec_mask >> table_of_key(pack, ntables, k0)) & 1u)
+                    ? 0u : cdiv_u32(se - ss, kChainTile);
         }
         uint32_t total;
         const uint32_t inc = block_inclusive_scan_1024(v, lds16, &total);
@@ -1482,89 +1489,333 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
     }
 }
 
-// Update phase, chain role: wave w takes items w, w + nwaves, ... of the cost-ordered
-// (column, 64-feature slice) list and applies the update of its slice.
+// Early chains.  The longest chains of a Zipf batch belong to the smallest tables (the
+// 3-row Criteo table's hottest column has 835 K occurrences: a ~3 ms chain), and a chain
+// planned from the sorted pairs cannot start before the whole index phase (~1 ms).  For a
+// table of at most kEcMaxRows rows the chains are planned straight from its index array,
+// on a side stream from the start of the call: the occurrences of column c in bag b are
+// a run of r(c, b) equal bags in the column's sorted list (the sort is stable and bags
+// are contiguous), so the column's entries are, in bag order, ceil(r / S) entries per
+// bag with r > 0 — the same entries k_chain_emit would cut from the sorted list.  Which
+// columns are chains (more than `chunk` occurrences) is decided from the same counts
+// (occurrences in [1, nrows]), so the main index phase skips exactly these columns
+// (k_chain_tiles) and the chunk pass never sees them (they are multi-chunk).
+constexpr int kEcMaxRows = 128;  // tables with at most this many rows
+constexpr int kEcBags = 256;     // bags per workgroup of k_ec_count / k_ec_emit
+constexpr int kEcMaxPool = 255;  // per-bag counts fit a byte
+constexpr int kEcMaxBatch = 1 << 20;
+constexpr int kEcStats = 8;      // per (column, block): occurrences, entries at S = 1..16
+
+struct EcList {
+    int n;                                        // early-chain tables
+    uint32_t mask;                                // bit t: table t is one of them
+    int t[ET_MAX_TABLES_PER_LAUNCH];              // their table indices
+    uint32_t blk0[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of bag blocks
+    uint32_t col0[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of nrows (EC columns)
+    uint32_t cb0[ET_MAX_TABLES_PER_LAUNCH + 1];   // prefix of blocks x nrows (stat records)
+};
+
+inline bool ec_table(const et_update_desc& d) {
+    return d.nrows > 0 && d.nrows <= kEcMaxRows && d.pool > 0 && d.pool <= kEcMaxPool &&
+           d.batch > 0 && d.batch <= kEcMaxBatch && d.dim > 0;
+}
+
+// Per-bag column counts in LDS: row `tid` (bag blk * kEcBags + tid) holds r(c, bag) for
+// the table's R <= kEcMaxRows columns, one byte each (out-of-range indices are not
+// counted; the main index phase reports them).
+__device__ __forceinline__ void ec_hist(const et_update_desc& d, uint32_t blk, uint8_t* hist,
+                                        uint32_t RS) {
+    const uint32_t R = (uint32_t)d.nrows, pool = (uint32_t)d.pool;
+    uint32_t* row = reinterpret_cast<uint32_t*>(hist + threadIdx.x * RS);
+    for (uint32_t i = 0; i < RS / 4; ++i) row[i] = 0u;
+    const int64_t b = (int64_t)blk * kEcBags + threadIdx.x;
+    if (b < d.batch) {
+        const int64_t* ip = d.idx + b * d.ld_idx;
+        uint8_t* h = hist + threadIdx.x * RS;
+        for (uint32_t j = 0; j < pool; ++j) {
+            const uint64_t c = (uint64_t)(ip[j] - 1);
+            if (c < R) h[c] = (uint8_t)(h[c] + 1u);
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int ec_find(const EcList& ec, uint32_t blk) {
+    int e = 0;
+    while (e + 1 < ec.n && blk >= ec.blk0[e + 1]) ++e;
+    return e;
+}
+
+// The columns of a block are summed by "parts": thread (c, p) = (tid % R, tid / R) walks
+// bags [p * len, (p + 1) * len) of the block for column c (nparts = kEcBags / R >= 2).
+struct EcParts {
+    uint32_t R, RS, nparts, len, c, p, b0, b1;
+    bool on;
+};
+
+__device__ __forceinline__ EcParts ec_parts(uint32_t R) {
+    EcParts q;
+    q.R = R;
+    q.RS = (R + 3u) & ~3u;
+    q.nparts = (uint32_t)kEcBags / R;
+    q.len = cdiv_u32((uint32_t)kEcBags, q.nparts);
+    q.on = threadIdx.x < q.nparts * R;
+    q.c = threadIdx.x % R;
+    q.p = threadIdx.x / R;
+    q.b0 = q.on ? q.p * q.len : 0u;
+    const uint32_t e = q.b0 + q.len;
+    q.b1 = q.on ? (e < (uint32_t)kEcBags ? e : (uint32_t)kEcBags) : 0u;
+    return q;
+}
+
+// EC step 1, one workgroup per (table, block of kEcBags bags): per column, its occurrences
+// in the block and the entries they make at S = 1, 2, 4, 8, 16.
+__global__ __launch_bounds__(256) void k_ec_count(UpdatePack pack, EcList ec,
+                                                  uint32_t* __restrict__ stats) {
+    __shared__ __attribute__((aligned(16))) uint8_t hist[kEcBags * kEcMaxRows];
+    __shared__ uint32_t red[kEcBags][6];
+    const int e = ec_find(ec, blockIdx.x);
+    const et_update_desc& d = pack.d[ec.t[e]];
+    const uint32_t blk = blockIdx.x - ec.blk0[e];
+    const uint32_t nblk = ec.blk0[e + 1] - ec.blk0[e];
+    const EcParts q = ec_parts((uint32_t)d.nrows);
+    ec_hist(d, blk, hist, q.RS);
+    uint32_t v[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+    for (uint32_t i = q.b0; i < q.b1; ++i) {
+        const uint32_t r = hist[i * q.RS + q.c];
+        v[0] += r;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[1 + k] += (r + (1u << k) - 1u) >> k;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) red[threadIdx.x][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x < q.R) {
+        uint32_t s6[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+        for (uint32_t p = 0; p < q.nparts; ++p)
+#pragma unroll
+            for (int k = 0; k < 6; ++k) s6[k] += red[p * q.R + threadIdx.x][k];
+        uint32_t* o = stats + (uint64_t)(ec.cb0[e] + threadIdx.x * nblk + blk) * kEcStats;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o[k] = s6[k];
+    }
+}
+
+// EC step 2, one wave per column: the totals, whether it is a chain (more than `chunk`
+// occurrences), its S (as k_chain_choose), padded entry count, entry offset (allocated
+// from counters[kCntT]: the layout depends on arrival order, the entries do not), the
+// per-block entry offsets at that S, the padding zeros and its descriptor.
+__global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uint32_t chunk,
+                                                 const uint32_t* __restrict__ stats,
+                                                 uint32_t* __restrict__ boff,
+                                                 uint32_t* __restrict__ cnt,
+                                                 uint2* __restrict__ info,
+                                                 ChainCol* __restrict__ chains,
+                                                 uint32_t* __restrict__ ent,
+                                                 uint32_t* __restrict__ counters) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t M = ec.col0[ec.n];
+    const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (g >= M) return;  // wave-uniform
+    int e = 0;
+    while (e + 1 < ec.n && g >= ec.col0[e + 1]) ++e;
+    const int t = ec.t[e];
+    const uint32_t c = g - ec.col0[e];
+    const uint32_t nblk = ec.blk0[e + 1] - ec.blk0[e];
+    const uint32_t* st = stats + (uint64_t)(ec.cb0[e] + c * nblk) * kEcStats;
+    uint32_t v[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+    for (uint32_t b = (uint32_t)lane; b < nblk; b += 64)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) v[k] += st[(uint64_t)b * kEcStats + k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = wave_sum_u32(v[k]);
+    int best = 0;
+    uint64_t bc = ~0ull;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint64_t cc = (uint64_t)v[1 + k] * (uint64_t)((1 << k) + kChainEntryCost);
+        if (cc < bc) bc = cc, best = k;
+    }
+    const bool is_chain = v[0] > chunk;  // wave-uniform
+    const uint32_t S = is_chain ? (1u << best) : 0u, E = is_chain ? v[1 + best] : 0u;
+    const uint32_t P = is_chain ? cdiv_u32(E, kChainGroup) * kChainGroup + kChainPad : 0u;
+    uint32_t e0 = 0;
+    if (lane == 0 && is_chain) e0 = atomicAdd(&counters[kCntT], P);
+    e0 = (uint32_t)__shfl((int)e0, 0, 64);
+    if (lane == 0) {
+        cnt[g] = P;
+        info[g] = make_uint2(S, E);
+        chains[g] = ChainCol{pack.row_off[t] + c, e0, is_chain ? (P - kChainPad) / kChainGroup : 0u,
+                             S};
+    }
+    if (!is_chain) return;
+    uint32_t carry = e0;  // per-block entry offsets at S, in block order
+    for (uint32_t b0 = 0; b0 < nblk; b0 += 64) {
+        const uint32_t b = b0 + (uint32_t)lane;
+        const uint32_t x = b < nblk ? st[(uint64_t)b * kEcStats + 1 + best] : 0u;
+        const uint32_t ex = wave_excl_scan_u32(x, lane);
+        if (b < nblk) boff[ec.cb0[e] + c * nblk + b] = carry + ex;
+        carry += wave_sum_u32(x);
+    }
+    for (uint32_t i = e0 + E + (uint32_t)lane; i < e0 + P; i += 64) ent[i] = 0u;
+}
+
+// EC step 3 (one workgroup): the cost order of the EC columns (as k_chain_plan) and their
+// count (counters[kCntM], read by the chain role).
+__global__ __launch_bounds__(1024) void k_ec_order(EcList ec, const uint2* __restrict__ info,
+                                                   uint32_t* __restrict__ order,
+                                                   uint32_t* __restrict__ counters) {
+    __shared__ uint32_t hist[65];
+    const uint32_t M = ec.col0[ec.n];
+    if (threadIdx.x < 65) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    auto bucket = [&](uint32_t g) {
+        const uint2 in = info[g];
+        const uint64_t cc = (uint64_t)in.y * (uint64_t)(in.x + kChainEntryCost);
+        return cc ? (uint32_t)__clzll((long long)cc) : 64u;
+    };
+    for (uint32_t g = threadIdx.x; g < M; g += 1024) atomicAdd(&hist[bucket(g)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < 65; ++k) {
+            const uint32_t h = hist[k];
+            hist[k] = run;
+            run += h;
+        }
+        counters[kCntM] = M;
+    }
+    __syncthreads();
+    for (uint32_t g = threadIdx.x; g < M; g += 1024) order[atomicAdd(&hist[bucket(g)], 1u)] = g;
+}
+
+// EC step 4, per (table, block): the entries of the block's bags for every chain column
+// at the column's block offset, in bag order: part (c, p) counts its bags' entries, the
+// parts of a column are scanned in LDS, then each part writes its bags' entries.
+__global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
+                                                 const uint32_t* __restrict__ boff,
+                                                 const uint2* __restrict__ info,
+                                                 uint32_t* __restrict__ ent) {
+    __shared__ __attribute__((aligned(16))) uint8_t hist[kEcBags * kEcMaxRows];
+    __shared__ uint32_t psum[kEcBags];
+    const int e = ec_find(ec, blockIdx.x);
+    const et_update_desc& d = pack.d[ec.t[e]];
+    const uint32_t blk = blockIdx.x - ec.blk0[e];
+    const uint32_t nblk = ec.blk0[e + 1] - ec.blk0[e];
+    const EcParts q = ec_parts((uint32_t)d.nrows);
+    ec_hist(d, blk, hist, q.RS);
+    const uint32_t S = q.on ? info[ec.col0[e] + q.c].x : 0u;
+    uint32_t mine = 0;
+    if (S)
+        for (uint32_t i = q.b0; i < q.b1; ++i) mine += cdiv_u32(hist[i * q.RS + q.c], S);
+    psum[threadIdx.x] = mine;
+    __syncthreads();
+    if (!S) return;  // no barrier below
+    uint32_t at = boff[ec.cb0[e] + q.c * nblk + blk];
+    for (uint32_t p = 0; p < q.p; ++p) at += psum[p * q.R + q.c];
+    for (uint32_t i = q.b0; i < q.b1; ++i) {
+        const uint32_t r = hist[i * q.RS + q.c];
+        const uint32_t k = cdiv_u32(r, S);
+        const uint32_t bag = blk * kEcBags + i;
+        for (uint32_t j = 0; j < k; ++j) chain_put(ent, at + j, j, k, r, S, bag);
+        at += k;
+    }
+}
+
+// Update phase, chain role: one (column, 64-feature slice) item of the cost-ordered list:
+// the serial sum of the slice's gradient columns and the update.
 template <int MODE, bool NT>
-__device__ __forceinline__ void sgd_chain_body(const UpdatePack& pack, int ntables,
-                                               const uint32_t* __restrict__ counters,
+__device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntables,
                                                const ChainCol* __restrict__ chains,
                                                const uint32_t* __restrict__ order,
                                                const uint32_t* __restrict__ ent, int ns,
-                                               float eta32, double eta64, uint32_t bid,
-                                               uint32_t nblk, bool plain) {
+                                               float eta32, double eta64, uint32_t it,
+                                               bool plain) {
     const int lane = threadIdx.x & 63;
-    // wave-uniform by construction; readfirstlane lets the compiler keep everything
-    // derived from it (the chain's entry pointer, its count) in SGPRs, as the asm needs
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t M = counters[kCntM];
-    const uint32_t nw = nblk * 4u, items = M * (uint32_t)ns;
-    // A chain issues a dependent VALU op about every 4.4 cycles, i.e. it alone nearly fills
-    // its SIMD's VALU: top priority, so the co-resident chunk-pass and singles waves (memory
-    // bound) take the leftover issue slots instead of stretching the critical chain.
+    const ChainCol c = chains[order[it / (uint32_t)ns]];
+    if (c.S == 0u) return;
+    const int t = table_of_key(pack, ntables, c.key);
+    const et_update_desc& d = pack.d[t];
+    const int f = (int)(it % (uint32_t)ns) * 64 + lane;
+    if ((int)(it % (uint32_t)ns) * 64 >= d.dim) return;  // uniform
+    const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
+    const uint32_t ld = (uint32_t)d.ld_delta;
+    // the gradient base as a wave-uniform (SGPR) pointer
+    const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
+    const float* delta = reinterpret_cast<const float*>(
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
+    const uint32_t* e = ent + c.e0;
+    float acc = 0.0f;
+    if (plain) {  // debug reference of the asm loop: the same adds, plainly
+        const uint32_t ne = c.ngr * kChainGroup;
+        for (uint32_t h = 0; h < ne; ++h) {
+            const uint32_t en = e[h];
+            const float x = delta[(uint64_t)(en & 0xffffffu) * ld + fc];
+            for (uint32_t k = 0; k < (en >> 24); ++k) acc = acc + x;
+        }
+    } else
+    switch (c.S) {
+        case 1: acc = chain_walk_asm<1>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+        case 2: acc = chain_walk_asm<2>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+        case 4: acc = chain_walk_asm<4>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+        case 8: acc = chain_walk_asm<8>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+        default: acc = chain_walk_asm<16>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+    }
+    if (f < d.dim) {
+        float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
+        store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+    }
+}
+
+// The chains of an update phase (early or regular), in their own launch on a side stream:
+// each wave takes the next item of the cost-ordered list from counters[kCntNext] (so the
+// longest chains start first and a late workgroup takes whatever is left), until the list
+// is exhausted.  A chain issues a dependent VALU op about every 4.4 cycles, i.e. it alone
+// nearly fills its SIMD's VALU, so two chains must not share a SIMD: the launch reserves
+// more than half of a CU's LDS (dynamic, untouched), so no other chain workgroup — of this
+// launch or the other chain launch — lands on the same CU, and the workgroup's 4 waves take
+// its 4 SIMDs.  Top priority: the co-resident chunk-pass / singles / index-phase waves
+// (memory bound) take the leftover issue slots.
+constexpr int kCntNext = 5;                        // counters slot: next chain item
+constexpr uint32_t kChainReserveLds = 82 * 1024;  // > 80 KiB: one chain workgroup per CU
+
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chains(
+    UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
+    const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64, int plain) {
+    extern __shared__ uint32_t reserve[];
+    (void)reserve;
+    const int lane = threadIdx.x & 63;
+    const uint32_t items = counters[kCntM] * (uint32_t)ns;
     __builtin_amdgcn_s_setprio(3);
-    for (uint32_t it = bid * 4u + (uint32_t)wave; it < items; it += nw) {
-        const ChainCol c = chains[order[it / (uint32_t)ns]];
-        if (c.S == 0u) continue;
-        const int t = table_of_key(pack, ntables, c.key);
-        const et_update_desc& d = pack.d[t];
-        const int f = (int)(it % (uint32_t)ns) * 64 + lane;
-        if ((int)(it % (uint32_t)ns) * 64 >= d.dim) continue;  // uniform
-        const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
-        const uint32_t ld = (uint32_t)d.ld_delta;
-        // the gradient base as a wave-uniform (SGPR) pointer
-        const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
-        const float* delta = reinterpret_cast<const float*>(
-            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
-            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
-        const uint32_t* e = ent + c.e0;
-        float acc = 0.0f;
-        if (plain) {  // debug reference of the asm loop: the same adds, plainly
-            const uint32_t ne = c.ngr * kChainGroup;
-            for (uint32_t h = 0; h < ne; ++h) {
-                const uint32_t en = e[h];
-                const float x = delta[(uint64_t)(en & 0xffffffu) * ld + fc];
-                for (uint32_t k = 0; k < (en >> 24); ++k) acc = acc + x;
-            }
-        } else
-        switch (c.S) {
-            case 1: acc = chain_walk_asm<1>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-            case 2: acc = chain_walk_asm<2>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-            case 4: acc = chain_walk_asm<4>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-            case 8: acc = chain_walk_asm<8>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-            default: acc = chain_walk_asm<16>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-        }
-        if (f < d.dim) {
-            float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
-            store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
-        }
+    for (;;) {
+        uint32_t it = 0;
+        if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
+        it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
+        if (it >= items) break;
+        sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it,
+                                 plain != 0);
     }
     __builtin_amdgcn_s_setprio(0);
 }
 
-// The whole update phase of an exact Float32 call in one launch: blocks [0, ncb) the
-// chains, [ncb, ncb + nch) the chunk pass over single-chunk columns of this capacity
-// group, the rest the single-occurrence columns.  D == 0: chains only (no vector table).
+// The rest of the update phase of an exact Float32 call in one launch: blocks [0, nch)
+// the chunk pass over single-chunk columns of this capacity group, the rest the
+// single-occurrence columns (the chains run in k_sgd_chains on the side streams).
 template <int D, int MODE, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_exact(
     UpdatePack pack, int ntables, const uint32_t* __restrict__ keys,
     const uint32_t* __restrict__ vals, const ChunkRec* __restrict__ recs,
     const uint32_t* __restrict__ counters, uint32_t sent, float eta32, double eta64,
-    uint32_t my_mask, const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, uint32_t ncb, uint32_t nch, int plain) {
-    if (blockIdx.x < ncb) {
-        sgd_chain_body<MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta32, eta64,
-                                 blockIdx.x, ncb, plain != 0);
-        return;
-    }
-    if constexpr (D > 0) {
-        if (blockIdx.x < ncb + nch)
-            sgd_chunks_body<D, MODE, NT>(pack, ntables, keys, vals, recs, counters, nullptr, 0,
-                                         sent, eta32, eta64, my_mask, 1, 1, blockIdx.x - ncb, nch);
-        else
-            sgd_singles_body<D, MODE, NT>(pack, ntables, vals, recs, counters, sent, eta32, eta64,
-                                          my_mask, blockIdx.x - ncb - nch,
-                                          gridDim.x - ncb - nch);
-    }
+    uint32_t my_mask, uint32_t nch) {
+    if (blockIdx.x < nch)
+        sgd_chunks_body<D, MODE, NT>(pack, ntables, keys, vals, recs, counters, nullptr, 0,
+                                     sent, eta32, eta64, my_mask, 1, 1, blockIdx.x, nch);
+    else
+        sgd_singles_body<D, MODE, NT>(pack, ntables, vals, recs, counters, sent, eta32, eta64,
+                                      my_mask, blockIdx.x - nch, gridDim.x - nch);
 }
 
 // Generic kernels (any dim / alignment / element type): one wave per chunk or
@@ -1665,6 +1916,12 @@ struct UpdateWs {
     // the index phase's tiles: first tile per column, tile -> column, entries per tile at
     // S = 1..16
     uint32_t *chain_tile0, *chain_tile_col, *chain_tcnt;
+    // early chains (EcList): per (column, block) stats and entry offsets, per EC column the
+    // padded entry count, (S, entries), descriptor and cost order, their entries, and a
+    // counter block (kCntM = EC columns) for the chain role
+    uint32_t *ec_stats, *ec_boff, *ec_cnt, *ec_order, *ec_ent, *ec_counters;
+    uint2* ec_info;
+    ChainCol* ec_chains;
     int64_t bytes;
 };
 
@@ -1679,7 +1936,8 @@ inline int64_t chain_tiles_max(int64_t n, uint32_t chunk) {
 // Lay out (or size, when base == nullptr) the update workspace for n occurrences and
 // partial rows of pdim floats.
 inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
-                                int nhot = 0, int64_t hot_batch = 0, int64_t hot_bytes = 0) {
+                                int nhot = 0, int64_t hot_batch = 0, int64_t hot_bytes = 0,
+                                const EcList* ec = nullptr, int64_t ec_occ = 0) {
     UpdateWs w;
     // every buffer 256-byte aligned whatever the caller's workspace alignment (the
     // 16-byte key / index / LDS-DMA loads rely on it): the layout starts at the first
@@ -1723,6 +1981,17 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
     w.chain_tile0 = (uint32_t*)take(4 * mmax);
     w.chain_tile_col = (uint32_t*)take(4 * tmax);
     w.chain_tcnt = (uint32_t*)take(20 * tmax);
+    {
+        const int64_t recs = ec && ec->n ? ec->cb0[ec->n] : 0, M = ec && ec->n ? ec->col0[ec->n] : 0;
+        w.ec_stats = (uint32_t*)take(4 * kEcStats * recs);
+        w.ec_boff = (uint32_t*)take(4 * recs);
+        w.ec_cnt = (uint32_t*)take(4 * M);
+        w.ec_order = (uint32_t*)take(4 * M);
+        w.ec_info = (uint2*)take(8 * M);
+        w.ec_chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * M);
+        w.ec_counters = (uint32_t*)take(4 * kCntSlots);
+        w.ec_ent = (uint32_t*)take(4 * (ec_occ + (int64_t)(kChainGroup + kChainPad) * M + 64));
+    }
     w.hot_nw = (int)((hot_batch + kHotWin - 1) / kHotWin);
     w.hot_hist = nullptr;
     w.hot_cnt = nullptr;
@@ -1768,7 +2037,7 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
 inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s,
                              uint32_t hot_mask = 0, const HotList* hl = nullptr,
-                             bool chain = false) {
+                             bool chain = false, uint32_t ec_mask = 0) {
     const int64_t blocks = cdiv64(n, 256);
     const unsigned kb_grid = (unsigned)(blocks < 65536 ? blocks : 65536);
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
@@ -1832,8 +2101,9 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
         const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
         const int64_t tmax = chain_tiles_max(n, chunk);
         const unsigned tg = (unsigned)(tmax < 8192 ? tmax : 8192);
-        hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, out.keys, w.seg_start,
-                           w.mlist, w.counters, sent, w.chain_tile0, w.chain_tile_col);
+        hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask,
+                           out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
+                           w.chain_tile_col);
         hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                            out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
                            w.chain_tile_col, w.chain_tcnt);
@@ -1910,41 +2180,63 @@ inline bool sgd_chunks_occ5() {
     return v;
 }
 
-// Workgroups of the exact mode's chain role: one item per (chain column, 64-feature slice),
-// cost-ordered; at most 256 workgroups (1024 waves: one per SIMD when spread one per CU)
-// so no two of the first round's chains, the longest, share a SIMD's VALU; the ~17 K
-// items of the config-4 batch take about 17 rounds, the later ones short.
-inline unsigned chain_blocks(int64_t n) {
-    const int64_t g = cdiv64(n, 65536);
-    return (unsigned)(g < 1 ? 1 : g > 256 ? 256 : g);
-}
+// The chains of an exact update phase: the side stream of the early chains (null: none)
+// and their column count, the side stream of the regular chains (forked from the caller's
+// stream after the index phase).
+struct ChainRun {
+    hipStream_t ec_side = nullptr;
+    uint32_t ec_ncols = 0;
+    hipStream_t side = nullptr;
+};
 
-// The update phase of an exact Float32 call: chains + chunk pass + singles in one launch
-// per capacity group (the chains ride in the first), then the generic tables' single-chunk
-// columns.  No partial sums, no combine.
+// k_sgd_chains on stream `s`: zero the item counter, at most `nb` workgroups.
 template <int MODE, bool NT>
-int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
-                     int64_t n, int pdim, uint32_t sent, float eta32, double eta64,
-                     const VecGroups& vg, bool any_generic, hipStream_t s, unsigned grid) {
-    const unsigned ncb = chain_blocks(n);
-    const int ns = (pdim + 63) / 64;
+int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
+                  const uint32_t* order, const uint32_t* ent, int ns, float eta32, double eta64,
+                  unsigned nb, hipStream_t s) {
     static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++
         const char* e = getenv("ET_CHAIN_ASM");
         return e && atoi(e) == 0 ? 1 : 0;
     }();
-    if (vg.n == 0)
-        hipLaunchKernelGGL((k_sgd_exact<0, MODE, NT>), dim3(ncb), dim3(256), 0, s, pack, ntables,
-                           gr.keys, gr.vals, w.recs, w.counters, sent, eta32, eta64, 0u, w.chains,
-                           w.chain_order, w.chain_ent, ns, ncb, 0u, plain);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&k_sgd_chains<MODE, NT>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
+    ET_HIP_CHECK(attr);
+    ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
+    hipLaunchKernelGGL((k_sgd_chains<MODE, NT>), dim3(nb), dim3(256), kChainReserveLds, s, pack,
+                       ntables, counters, chains, order, ent, ns, eta32, eta64, plain);
+    ET_LAUNCH_CHECK("k_sgd_chains");
+    return ET_OK;
+}
+
+// The update phase of an exact Float32 call: the early chains (side stream 1, already
+// planned) and the regular chains (side stream 2) in k_sgd_chains, the chunk pass over
+// single-chunk columns + the singles in one launch per capacity group on the caller's
+// stream, then the generic tables' single-chunk columns.  No partial sums, no combine.
+template <int MODE, bool NT>
+int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
+                     int64_t n, int pdim, uint32_t sent, float eta32, double eta64,
+                     const VecGroups& vg, bool any_generic, hipStream_t s, unsigned grid,
+                     ChainRun cr) {
+    const int ns = (pdim + 63) / 64;
+    int rc;
+    if (cr.ec_side) {
+        const int64_t items = (int64_t)cr.ec_ncols * ns;
+        const unsigned eb = (unsigned)(cdiv64(items, 4) < 256 ? cdiv64(items, 4) : 256);
+        rc = launch_chains<MODE, NT>(pack, ntables, w.ec_counters, w.ec_chains, w.ec_order,
+                                     w.ec_ent, ns, eta32, eta64, eb, cr.ec_side);
+        if (rc != ET_OK) return rc;
+    }
+    rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order, w.chain_ent,
+                                 ns, eta32, eta64, 256u, cr.side);
+    if (rc != ET_OK) return rc;
 #define ET_SGD_EXACT(DD)                                                                       \
     case DD:                                                                                   \
-        hipLaunchKernelGGL((k_sgd_exact<DD, MODE, NT>), dim3(nc + 2 * grid), dim3(256), 0, s,  \
-                           pack, ntables, gr.keys, gr.vals, w.recs, w.counters, sent, eta32,   \
-                           eta64, vg.mask[i], w.chains, w.chain_order, w.chain_ent, ns, nc,    \
-                           grid, plain);                                                       \
+        hipLaunchKernelGGL((k_sgd_exact<DD, MODE, NT>), dim3(2 * grid), dim3(256), 0, s, pack, \
+                           ntables, gr.keys, gr.vals, w.recs, w.counters, sent, eta32, eta64,  \
+                           vg.mask[i], grid);                                                  \
         break;
     for (int i = 0; i < vg.n; ++i) {
-        const unsigned nc = i == 0 ? ncb : 0u;
         switch (vg.cap[i]) {
             ET_SGD_EXACT(16)
             ET_SGD_EXACT(32)
@@ -1972,11 +2264,11 @@ template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
                      const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl, unsigned grid, bool chain, int64_t n) {
+                     const HotList& hl, unsigned grid, bool chain, int64_t n, ChainRun cr) {
     if constexpr (__is_same(T, float)) {
         if (chain)
             return launch_sgd_exact<MODE, NT>(pack, ntables, gr, w, n, pdim, sent, eta_c, eta64, vg,
-                                              any_generic, s, grid);
+                                              any_generic, s, grid, cr);
         const bool singles = sgd_singles();
         // combine workgroups of k_sgd_tail: a quarter of one resident wave of workgroups,
         // so the singles start at once beside them
@@ -2061,10 +2353,11 @@ template <typename T, typename C>
 int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, double eta_c, double eta64,
                      int mode, bool nt, const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl, unsigned grid, bool chain = false, int64_t n = 0) {
+                     const HotList& hl, unsigned grid, bool chain = false, int64_t n = 0,
+                     ChainRun cr = ChainRun{}) {
 #define ET_SGD_CALL(M, NTV)                                                                \
     return launch_sgd_typed<T, C, M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, (C)eta_c, \
-                                          eta64, vg, any_generic, s, hl, grid, chain, n)
+                                          eta64, vg, any_generic, s, hl, grid, chain, n, cr)
     if (mode == 0) {
         if (nt) ET_SGD_CALL(0, true);
         ET_SGD_CALL(0, false);
@@ -2142,6 +2435,116 @@ inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_
     return ET_OK;
 }
 
+// Early-chain tables of these descriptors (ec_table) and their occurrences; the list
+// sizes the workspace whatever the flags, and et_sparse_sgd uses it in exact Float32 mode.
+inline EcList ec_list(const et_update_desc* descs, int ntables, int64_t* occ) {
+    EcList ec;
+    ec.n = 0;
+    ec.mask = 0;
+    ec.blk0[0] = ec.col0[0] = ec.cb0[0] = 0;
+    *occ = 0;
+    for (int t = 0; t < ntables; ++t) {
+        const et_update_desc& d = descs[t];
+        if (!ec_table(d)) continue;
+        const uint32_t nb = (uint32_t)cdiv64(d.batch, kEcBags);
+        ec.t[ec.n] = t;
+        ec.mask |= 1u << t;
+        ec.blk0[ec.n + 1] = ec.blk0[ec.n] + nb;
+        ec.col0[ec.n + 1] = ec.col0[ec.n] + (uint32_t)d.nrows;
+        ec.cb0[ec.n + 1] = ec.cb0[ec.n] + nb * (uint32_t)d.nrows;
+        *occ += d.pool * d.batch;
+        ++ec.n;
+    }
+    return ec;
+}
+
+// ET_EC=0 plans every chain from the sorted pairs (experiments).
+inline bool ec_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("ET_EC");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
+// Two side streams per device (highest priority) for the exact mode's chains: stream 0
+// takes the early chains (forked from the caller's stream at the start of the call), stream
+// 1 the regular ones (forked after the index phase).  Both are joined back into the
+// caller's stream inside the same library call, so a HIP graph capture of the caller's
+// stream captures every branch.  The fork/join events are shared, so a call that uses
+// the side streams holds `mu` from its first fork to its last join.
+struct SideStreams {
+    std::mutex mu;
+    hipStream_t st[2] = {nullptr, nullptr};
+    hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+};
+
+inline SideStreams* side_streams() {
+    static SideStreams streams[64];
+    static std::mutex init_mu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStreams& ss = streams[dev];
+    std::lock_guard<std::mutex> lk(init_mu);
+    if (!ss.st[1]) {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
+        for (int i = 0; i < 2; ++i)
+            if ((!ss.fork[i] && hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming)) ||
+                (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
+                (!ss.st[i] && hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking,
+                                                          greatest)))
+                return nullptr;
+    }
+    return &ss;
+}
+
+// fork(i): side stream i waits for everything the caller's stream has queued so far;
+// the destructor joins every forked side stream (every return path of et_sparse_sgd).
+struct SideFork {
+    SideStreams* ss = nullptr;
+    hipStream_t main = nullptr;
+    std::unique_lock<std::mutex> lk;
+    bool forked[2] = {false, false};
+    SideFork(SideStreams* s, hipStream_t m) : ss(s), main(m) {
+        if (ss) lk = std::unique_lock<std::mutex>(ss->mu);
+    }
+    hipStream_t fork(int i) {
+        if (!ss) return nullptr;
+        if (!forked[i]) {
+            if (hipEventRecord(ss->fork[i], main) != hipSuccess ||
+                hipStreamWaitEvent(ss->st[i], ss->fork[i], 0) != hipSuccess)
+                return nullptr;
+            forked[i] = true;
+        }
+        return ss->st[i];
+    }
+    ~SideFork() {
+        for (int i = 0; i < 2; ++i)
+            if (forked[i]) {
+                (void)hipEventRecord(ss->join[i], ss->st[i]);
+                (void)hipStreamWaitEvent(main, ss->join[i], 0);
+            }
+    }
+};
+
+// The early-chain plan (k_ec_count -> k_ec_plan -> k_ec_emit) on stream `s`.
+inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chunk,
+                          const UpdateWs& w, hipStream_t s) {
+    const uint32_t M = ec.col0[ec.n];
+    ET_HIP_CHECK(hipMemsetAsync(w.ec_counters, 0, 4 * kCntSlots, s));
+    hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_stats);
+    hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
+                       w.ec_stats, w.ec_boff, w.ec_cnt, w.ec_info, w.ec_chains, w.ec_ent,
+                       w.ec_counters);
+    hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.ec_info, w.ec_order,
+                       w.ec_counters);
+    hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_boff,
+                       w.ec_info, w.ec_ent);
+    ET_LAUNCH_CHECK("k_ec_emit");
+    return ET_OK;
+}
+
 }  // namespace et
 
 // ---------------------------------------------------------------------------
@@ -2160,7 +2563,9 @@ extern "C" int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntable
     int nhot;
     int64_t hb, hbytes;
     et::hot_sizes(descs, ntables, &nhot, &hb, &hbytes);
-    *bytes = et::carve_update_ws(nullptr, n, pdim, et::kChunk, nhot, hb, hbytes).bytes;
+    int64_t ec_occ;
+    const et::EcList ec = et::ec_list(descs, ntables, &ec_occ);
+    *bytes = et::carve_update_ws(nullptr, n, pdim, et::kChunk, nhot, hb, hbytes, &ec, ec_occ).bytes;
     return ET_OK;
 }
 
@@ -2196,8 +2601,10 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     int64_t hb, hbytes;
     uint64_t soff[ET_MAX_TABLES_PER_LAUNCH];
     et::hot_sizes(descs, ntables, &nhot, &hb, &hbytes, soff);
+    int64_t ec_occ;
+    const et::EcList ec = et::ec_list(descs, ntables, &ec_occ);
     et::UpdateWs w = et::carve_update_ws(static_cast<char*>(workspace), n, pdim, et::kChunk,
-                                         nhot, hb, hbytes);
+                                         nhot, hb, hbytes, &ec, ec_occ);
     if (!workspace || ws_bytes < w.bytes)
         return et::fail(ET_ERR_WORKSPACE, "workspace of %lld bytes needed",
                         (long long)w.bytes);
@@ -2249,12 +2656,36 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
             hl.soff[hl.n] = soff[t];
             hl.t[hl.n++] = t;
         }
+    // exact Float32: the chains run on two side streams — the early chains (small tables,
+    // planned from the index arrays at the start of the index phase) from the start of the
+    // call, the regular ones once the index phase has planned them
+    const bool use_ec = chain && ec.n > 0 && et::ec_enabled();
+    et::SideStreams* sides = chain ? et::side_streams() : nullptr;
+    if (chain && !sides) return et::fail(ET_ERR_HIP, "sparse SGD: side streams unavailable");
+    et::SideFork fork(sides, s);
+    hipStream_t ec_side = nullptr;
+    if (use_ec) {
+        ec_side = fork.fork(0);
+        if (!ec_side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
+        if (!apply_only) {
+            rc = et::launch_ec_plan(pack, ec, chunk, w, ec_side);
+            if (rc != ET_OK) return rc;
+        }
+    }
     et::Grouped gr;
     if (apply_only) {
         gr = et::grouped_pairs(pack, ntables, w);  // phase 1 ran earlier in stream order
     } else {
-        rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s, hot_mask, &hl, chain);
+        rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s, hot_mask, &hl, chain,
+                                   use_ec ? ec.mask : 0u);
         if (rc != ET_OK || index_only) return rc;
+    }
+    et::ChainRun cr;
+    if (chain) {
+        cr.ec_side = ec_side;
+        cr.ec_ncols = use_ec ? ec.col0[ec.n] : 0u;
+        cr.side = fork.fork(1);  // after the index phase
+        if (!cr.side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
     }
 
     const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
@@ -2265,7 +2696,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         case ET_F32:
             return et::launch_sgd_dtype<float, float>(pack, ntables, gr, w, chunk, pdim, sent,
                                                       eta_c, eta, mode, nt, vg,
-                                                      any_generic, s, hl, grid, chain, n);
+                                                      any_generic, s, hl, grid, chain, n, cr);
         case ET_F64:
             return et::launch_sgd_dtype<double, double>(pack, ntables, gr, w, chunk, pdim, sent,
                                                          eta_c, eta, mode, nt, vg,

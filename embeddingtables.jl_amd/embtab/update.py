@@ -372,10 +372,11 @@ def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
                   telemetry_cb=None, indexers=None, hot_pass: bool = False):
     """src/sparseupdate.jl:199-238: index every table, ``telemetry_cb()``, then update
     every table.  Both phases are one device pipeline per (path, eltype) group of at
-    most ET_MAX_TABLES_PER_LAUNCH tables (ET_FLAG_SGD_INDEX_ONLY, then
-    ET_FLAG_SGD_APPLY_ONLY from the same workspace); ``telemetry_cb`` runs on the host
-    once the index phase is enqueued (stream order puts it between the phases, as the
-    reference's call between its two threaded loops).  ``indexers[i]`` receives table
+    most ET_MAX_TABLES_PER_LAUNCH tables; with a ``telemetry_cb`` they are two calls
+    (ET_FLAG_SGD_INDEX_ONLY for every group, the callback on the host once they are
+    enqueued — stream order puts it between the phases, as the reference's call between
+    its two threaded loops — then ET_FLAG_SGD_APPLY_ONLY from the same workspaces),
+    without one a single call per group.  ``indexers[i]`` receives table
     i's Indexer (built from ``grads[i].indices`` on first use — see Indexer._defer).
     ``num_splits`` / ``nthreads`` / ``scratchspaces`` only shape the reference's CPU work
     queue and have no device counterpart."""
@@ -409,20 +410,25 @@ def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool,
                                                    ctypes.byref(nb)))
                 ws = _workspace(nb.value, dev, f"sgd{len(calls)}")
                 calls.append((_lib.TORCH_TO_ET[dtype], arr, len(part), flags, ws))
+        # Without a telemetry callback nothing observes the phase boundary, so each group
+        # runs both phases in one call: the same device work in the same stream order
+        # (bit-identical), and the exact mode's early chains (small tables, planned from the
+        # index arrays) start with the call instead of after every group's index phase.
+        phased = telemetry_cb is not None
         for et_t, arr, n, flags, ws in calls:  # phase 1: index all tables
             _lib.check(L.et_sparse_sgd(et_t, ctypes.addressof(arr), n, float(opt.eta),
-                                       flags | _lib.ET_FLAG_SGD_INDEX_ONLY, ws.data_ptr(),
-                                       ws.numel(), stream))
+                                       flags | (_lib.ET_FLAG_SGD_INDEX_ONLY if phased else 0),
+                                       ws.data_ptr(), ws.numel(), stream))
     if indexers is not None:
         for ix, A, g in zip(indexers, tables, grads):
             if isinstance(ix, Indexer):
                 ix._defer(g.indices, A.size()[1])
     if telemetry_cb is not None:
         telemetry_cb()
-    for et_t, arr, n, flags, ws in calls:  # phase 2: update all tables
-        _lib.check(L.et_sparse_sgd(et_t, ctypes.addressof(arr), n, float(opt.eta),
-                                   flags | _lib.ET_FLAG_SGD_APPLY_ONLY, ws.data_ptr(),
-                                   ws.numel(), stream))
+        for et_t, arr, n, flags, ws in calls:  # phase 2: update all tables
+            _lib.check(L.et_sparse_sgd(et_t, ctypes.addressof(arr), n, float(opt.eta),
+                                       flags | _lib.ET_FLAG_SGD_APPLY_ONLY, ws.data_ptr(),
+                                       ws.numel(), stream))
 
 
 def _update_from_indexer(table, grad: SparseEmbeddingUpdate, indexer: AbstractIndexer,

@@ -406,7 +406,7 @@ end
 # src/sparseupdate.jl:199-238: index all tables, telemetry_cb(), update all tables.
 # One device pipeline per (path, eltype) group, split at the same boundary
 # (ET_FLAG_SGD_INDEX_ONLY, then ET_FLAG_SGD_APPLY_ONLY from the same workspace);
-# telemetry_cb runs once the index phase is enqueued.  indexers[i] receives table i's
+# telemetry_cb (if given) runs once the index phase is enqueued.  indexers[i] receives table i's
 # Indexer in the index phase as the reference's does: a HipIndexer is built on the device
 # (et_index_build, stream-ordered, no host work).  A host Indexer is filled by the
 # reference's own serial index! on a downloaded copy of the indices only when asked for
@@ -416,7 +416,7 @@ const WORKSPACES = Dict{Int,Any}()
 function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  grads::AbstractVector{<:SparseEmbeddingUpdate},
                  indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
-                 telemetry_cb = Returns(nothing), fill_host_indexers::Bool = false,
+                 telemetry_cb = nothing, fill_host_indexers::Bool = false,
                  exact::Bool = EXACT[], kw...) where {Nontemporal}
     nt = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
          (exact ? ET_FLAG_EXACT_UPDATE : UInt32(0))
@@ -447,7 +447,10 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                     et_dtype(T), descs, length(descs), Float64(opt.eta), flags | phase, ws.ptr,
                     length(ws), stream()))
     end
-    run(ET_FLAG_SGD_INDEX_ONLY)
+    # without a callback nothing observes the phase boundary: one call per group (the
+    # same device work and order; exact mode's early chains start with the call)
+    phased = telemetry_cb !== nothing
+    run(phased ? ET_FLAG_SGD_INDEX_ONLY : UInt32(0))
     for i in eachindex(indexers, grads)
         if indexers[i] isa HipIndexer
             index!(indexers[i], grads[i].indices, size(tables[i], 2))
@@ -455,8 +458,10 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
             EmbeddingTables.index!(indexers[i], download(grads[i].indices), size(tables[i], 2))
         end
     end
-    telemetry_cb()
-    run(ET_FLAG_SGD_APPLY_ONLY)
+    if phased
+        telemetry_cb()
+        run(ET_FLAG_SGD_APPLY_ONLY)
+    end
     return nothing
 end
 
