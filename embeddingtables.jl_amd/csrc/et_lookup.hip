@@ -467,6 +467,8 @@ constexpr int kXcds = 8;
 struct StripeMap {
     uint32_t entry[kXcds][ET_MAX_TABLES_PER_LAUNCH];
     uint32_t ntload_mask;  // bit t: non-temporal row loads for table t
+    uint32_t prio_mask;    // bit t: table t's waves run at raised issue priority
+    int prio;
 };
 
 template <typename T, typename A, int D, int U, bool NT, bool NTI, bool SG = false>
@@ -482,6 +484,7 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
     const int t = (int)(e & 0xff);
     const int64_t chunk = (int64_t)(e >> 8) * stripe_chunks + j;
     if (j >= stripe_chunks || chunk >= nchunks) return;
+    if ((sm.prio_mask >> t) & 1u) __builtin_amdgcn_s_setprio(2);
     if constexpr (SG) {
         if ((sm.ntload_mask >> t) & 1u)
             run_bags_s<T, A, U, NT, true>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
@@ -666,6 +669,7 @@ struct LookupTuning {
     int rows_in_flight = 0;        // ET_U=4|8|16: rows per group in flight (fp32 D=128)
     int w8 = 0;                    // ET_W8=1: the striped kernel held to 8 waves per SIMD
     int sgpr = 1;                  // ET_SGPR=0: 512-byte rows use the per-lane loop too
+    int heavy_prio = 0;            // ET_HEAVY_PRIO=1: heavy tables' waves at priority 2
 };
 
 inline const LookupTuning& tuning() {
@@ -680,6 +684,7 @@ inline const LookupTuning& tuning() {
         if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
         if (const char* e = getenv("ET_W8")) v.w8 = atoi(e);
         if (const char* e = getenv("ET_SGPR")) v.sgpr = atoi(e);
+        if (const char* e = getenv("ET_HEAVY_PRIO")) v.heavy_prio = atoi(e);
         return v;
     }();
     return t;
@@ -695,10 +700,12 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
     int nh = 0, nl = 0;
     int64_t bytes[ET_MAX_TABLES_PER_LAUNCH];
     sm.ntload_mask = 0;
+    sm.prio_mask = 0;
     for (int t = 0; t < n; ++t) {
         bytes[t] = pack.d[t].nrows * pack.d[t].ld_table * es;
         if (bytes[t] > tu.light_bytes) {
             heavy[nh++] = t;
+            if (tu.heavy_prio) sm.prio_mask |= 1u << t;
             if (tu.ntload && bytes[t] > tu.ntload_bytes) sm.ntload_mask |= 1u << t;
         } else {
             light[nl++] = t;

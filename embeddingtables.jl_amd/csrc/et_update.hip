@@ -43,7 +43,11 @@ struct UpdatePack {
 };
 
 // Counters in the workspace.
-enum { kCntU = 0, kCntC = 1, kCntM = 2, kCntT = 3, kCntSlots = 16 };
+enum { kCntU = 0, kCntC = 1, kCntM = 2, kCntT = 3,
+       kCntNext = 5,     // next plain chain item (k_sgd_chains)
+       kCntHfNext = 6,   // next helper-fed chain item
+       kCntHfItems = 7,  // helper-fed items (the first of the chain order)
+       kCntSlots = 16 };
 
 __device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, uint32_t key) {
     int t = 0;
@@ -1098,9 +1102,16 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
 // launch, so the hottest chains (834,828 adds on the config-4 batch) overlap the rest.
 constexpr int kChainGroup = kChainAsmTrip;  // entries per trip of the asm loop
 constexpr int kChainPad = kChainAsmPad;     // readable entries past the last trip
-constexpr int kChainEntryCost = kChainAsmEntryCost;  // issue slots per entry beside the fmas
+// Issue slots of one entry of a chain at S adds per entry, doubled (et_chain_asm.h:
+// readlane, address, load and half a wait, then S = 1: the add; S = 2, 4 (the 64-deep
+// loop): a second readlane, the mask's compare and select and S masked fmas; S = 8, 16
+// (the 32-deep loop): the mask and S masked fmas).
+__host__ __device__ constexpr uint32_t chain_entry_cost2(uint32_t S) {
+    return S <= 1u ? 9u : S <= 4u ? 2u * S + 13u : 2u * S + 11u;
+}
 
-// A chain entry: r adds (r <= 16) of gradient column `bag` (< 2^24); 0 = padding.
+// A chain entry: r adds (r <= 16) of gradient column `bag` (< 2^24); padding is r = 0 at
+// bag = batch (past the gradient: the chain loop's range-checked load returns +0).
 __device__ __forceinline__ uint32_t chain_entry(uint32_t r, uint32_t bag) {
     return r << 24 | bag;
 }
@@ -1320,7 +1331,7 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             E[k] = wave_sum_u32(E[k]);
-            const uint64_t c = (uint64_t)E[k] * (uint64_t)((1 << k) + kChainEntryCost);
+            const uint64_t c = (uint64_t)E[k] * chain_entry_cost2(1u << k);
             if (c < bc) bc = c, best = k;
         }
         if (lane == 0) {
@@ -1346,7 +1357,7 @@ __global__ __launch_bounds__(1024) void k_chain_plan(const uint32_t* __restrict_
     __syncthreads();
     auto bucket = [&](uint32_t m) {  // leading zeros of the cost: 0 = costliest, 64 = none
         const uint2 in = info[m];
-        const uint64_t c = (uint64_t)in.y * (uint64_t)(in.x + kChainEntryCost);
+        const uint64_t c = (uint64_t)in.y * chain_entry_cost2(in.x);
         return c ? (uint32_t)__clzll((long long)c) : 64u;
     };
     uint32_t carry = 0;
@@ -1444,7 +1455,8 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
         }
         if (c.ti + 1 == c.nt) {
             const uint32_t e0 = e0s[c.m], P = cnt[c.m];
-            for (uint32_t i = e0 + in.y + threadIdx.x; i < e0 + P; i += 256) ent[i] = 0u;
+            const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[c.t].batch);
+            for (uint32_t i = e0 + in.y + threadIdx.x; i < e0 + P; i += 256) ent[i] = pad;
             if (threadIdx.x == 0)
                 chains[c.m] = ChainCol{keys[c.ss], e0, (P - kChainPad) / kChainGroup, S};
         }
@@ -1477,7 +1489,8 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
         if (P != c.ngr * kChainGroup + kChainPad || c.S != info[m].x) bad = 1;
         for (uint32_t i = lane; i < P; i += 64) {
             const uint32_t e = ent[c.e0 + i], r = e >> 24;
-            const bool ok = (uint64_t)(e & 0xffffffu) < lim && r <= c.S;
+            const bool ok = ((uint64_t)(e & 0xffffffu) < lim || (r == 0u && (e & 0xffffffu) == lim)) &&
+                            r <= c.S;
             if (!ok) ent[c.e0 + i] = 0u;
             bad += ok ? 0u : 1u;
             real += (ok && r > 0u) ? 1u : 0u;
@@ -1505,6 +1518,7 @@ constexpr int kEcBags = 256;     // bags per workgroup of k_ec_count / k_ec_emit
 constexpr int kEcMaxPool = 255;  // per-bag counts fit a byte
 constexpr int kEcMaxBatch = 1 << 20;
 constexpr int kEcStats = 8;      // per (column, block): occurrences, entries at S = 1..16
+constexpr uint32_t kHfMinOcc = 65536;  // helper-fed chains: at least this many occurrences
 
 struct EcList {
     int n;                                        // early-chain tables
@@ -1609,6 +1623,7 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
                                                  const uint32_t* __restrict__ stats,
                                                  uint32_t* __restrict__ boff,
                                                  uint32_t* __restrict__ cnt,
+                                                 uint32_t* __restrict__ nocc,
                                                  uint2* __restrict__ info,
                                                  ChainCol* __restrict__ chains,
                                                  uint32_t* __restrict__ ent,
@@ -1633,7 +1648,7 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
     uint64_t bc = ~0ull;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        const uint64_t cc = (uint64_t)v[1 + k] * (uint64_t)((1 << k) + kChainEntryCost);
+        const uint64_t cc = (uint64_t)v[1 + k] * chain_entry_cost2(1u << k);
         if (cc < bc) bc = cc, best = k;
     }
     const bool is_chain = v[0] > chunk;  // wave-uniform
@@ -1644,6 +1659,7 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
     e0 = (uint32_t)__shfl((int)e0, 0, 64);
     if (lane == 0) {
         cnt[g] = P;
+        nocc[g] = v[0];
         info[g] = make_uint2(S, E);
         chains[g] = ChainCol{pack.row_off[t] + c, e0, is_chain ? (P - kChainPad) / kChainGroup : 0u,
                              S};
@@ -1657,28 +1673,33 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
         if (b < nblk) boff[ec.cb0[e] + c * nblk + b] = carry + ex;
         carry += wave_sum_u32(x);
     }
-    for (uint32_t i = e0 + E + (uint32_t)lane; i < e0 + P; i += 64) ent[i] = 0u;
+    const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[t].batch);
+    for (uint32_t i = e0 + E + (uint32_t)lane; i < e0 + P; i += 64) ent[i] = pad;
 }
 
 // EC step 3 (one workgroup): the cost order of the EC columns (as k_chain_plan) and their
 // count (counters[kCntM], read by the chain role).
 __global__ __launch_bounds__(1024) void k_ec_order(EcList ec, const uint2* __restrict__ info,
+                                                   const uint32_t* __restrict__ nocc, int ns,
                                                    uint32_t* __restrict__ order,
                                                    uint32_t* __restrict__ counters) {
-    __shared__ uint32_t hist[65];
+    __shared__ uint32_t hist[66];
     const uint32_t M = ec.col0[ec.n];
-    if (threadIdx.x < 65) hist[threadIdx.x] = 0u;
+    if (threadIdx.x < 66) hist[threadIdx.x] = 0u;
     __syncthreads();
+    // bucket 0: the helper-fed columns (long runs, many occurrences); then by log2 cost
     auto bucket = [&](uint32_t g) {
         const uint2 in = info[g];
-        const uint64_t cc = (uint64_t)in.y * (uint64_t)(in.x + kChainEntryCost);
-        return cc ? (uint32_t)__clzll((long long)cc) : 64u;
+        if (in.x >= 8u && nocc[g] >= kHfMinOcc) return 0u;
+        const uint64_t cc = (uint64_t)in.y * chain_entry_cost2(in.x);
+        return cc ? 1u + (uint32_t)__clzll((long long)cc) : 65u;
     };
     for (uint32_t g = threadIdx.x; g < M; g += 1024) atomicAdd(&hist[bucket(g)], 1u);
     __syncthreads();
     if (threadIdx.x == 0) {
+        counters[kCntHfItems] = hist[0] * (uint32_t)ns;
         uint32_t run = 0;
-        for (int k = 0; k < 65; ++k) {
+        for (int k = 0; k < 66; ++k) {
             const uint32_t h = hist[k];
             hist[k] = run;
             run += h;
@@ -1751,16 +1772,20 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
         const uint32_t ne = c.ngr * kChainGroup;
         for (uint32_t h = 0; h < ne; ++h) {
             const uint32_t en = e[h];
+            if ((en >> 24) == 0u) continue;  // padding
             const float x = delta[(uint64_t)(en & 0xffffffu) * ld + fc];
             for (uint32_t k = 0; k < (en >> 24); ++k) acc = acc + x;
         }
-    } else
-    switch (c.S) {
-        case 1: acc = chain_walk_asm<1>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-        case 2: acc = chain_walk_asm<2>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-        case 4: acc = chain_walk_asm<4>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-        case 8: acc = chain_walk_asm<8>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
-        default: acc = chain_walk_asm<16>(e, c.ngr, delta, 4u * fc, 4u * ld, 0.0f); break;
+    } else {
+        // range batch * ld * 4 bytes: a padding entry (bag = batch) loads +0
+        const i32x4 rs = chain_rsrc(delta, (uint32_t)d.batch * ld * 4u);
+        switch (c.S) {
+            case 1: acc = chain_walk_asm<1>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+            case 2: acc = chain_walk_asm<2>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+            case 4: acc = chain_walk_asm<4>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+            case 8: acc = chain_walk_asm<8>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+            default: acc = chain_walk_asm<16>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+        }
     }
     if (f < d.dim) {
         float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
@@ -1777,26 +1802,194 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
 // launch or the other chain launch — lands on the same CU, and the workgroup's 4 waves take
 // its 4 SIMDs.  Top priority: the co-resident chunk-pass / singles / index-phase waves
 // (memory bound) take the leftover issue slots.
-constexpr int kCntNext = 5;                        // counters slot: next chain item
-constexpr uint32_t kChainReserveLds = 82 * 1024;  // > 80 KiB: one chain workgroup per CU
+constexpr uint32_t kChainReserveLds = 84 * 1024;  // > 80 KiB: one chain workgroup per CU
 
+// Helper-fed chains ("HF": the longest early chains, whose runs are long — S >= 8 — and
+// whose columns have at least kHfMinOcc occurrences).  The plain loop spends, per entry of
+// r <= S adds, S masked fmacs and ~6 slots of address, load and mask work in the chain's
+// own wave.  Here a pair of waves shares one item: the helper wave loads each entry's
+// gradient column (lane = feature) and writes it r times into a transposed LDS ring (row
+// = feature, one slot per OCCURRENCE); the consumer wave reads 4 occurrences of its
+// feature per ds_read_b128 and adds them — exactly the reference's serial sum, one add per
+// occurrence, no masks.  The helper writes 16 copies from the entry's first slot (8
+// ds_write2): copies past r are overwritten by the next entry's (the helper writes in
+// order), and ring wrap-around gets a second write; slots are published to the consumer
+// only once valid (`produced`), and a slot is rewritten only once consumed (`consumed`).
+constexpr uint32_t kHfRing = 128;               // logical slots (power of two)
+constexpr uint32_t kHfRow = kHfRing + 32 + 4;   // 16 slack slots each side + bank pad
+constexpr uint32_t kHfK = 16;                   // entries per helper batch (2 in flight)
+constexpr uint32_t kHfWg = 24;                  // HF workgroups (2 pairs each) per launch
+
+struct HfCtl {
+    uint32_t seq, item, produced, consumed;
+};
+
+template <int MODE, bool NT>
+__device__ void hf_pair(const UpdatePack& pack, int ntables, uint32_t* __restrict__ counters,
+                        const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
+                        const uint2* __restrict__ info, const uint32_t* __restrict__ nocc,
+                        const uint32_t* __restrict__ ent, int ns, float eta32, double eta64,
+                        float* __restrict__ ring, volatile HfCtl* ctl, bool consumer) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t items = counters[kCntHfItems];
+    float* row = ring + lane * kHfRow + 16;  // this lane's feature row, logical slot 0
+    uint32_t seen = 0;
+    for (;;) {
+        uint32_t it;
+        if (consumer) {
+            it = 0;
+            if (lane == 0) it = atomicAdd(&counters[kCntHfNext], 1u);
+            it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
+            if (lane == 0) {
+                ctl->produced = 0u;
+                ctl->consumed = 0u;
+                ctl->item = it;
+                ctl->seq = seen + 1u;  // in order after the fields (one wave's LDS writes)
+            }
+            ++seen;
+        } else {
+            while (ctl->seq == seen) __builtin_amdgcn_s_sleep(1);
+            ++seen;
+            it = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl->item);
+        }
+        if (it >= items) return;
+        const uint32_t g = order[it / (uint32_t)ns];
+        const ChainCol c = chains[g];
+        const int t = table_of_key(pack, ntables, c.key);
+        const et_update_desc& d = pack.d[t];
+        const int slice = (int)(it % (uint32_t)ns);
+        if (c.S == 0u || slice * 64 >= d.dim) continue;  // both waves skip the item
+        const int f = slice * 64 + lane;
+        const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
+        const uint32_t n = nocc[g];
+        if (consumer) {
+            float acc = 0.0f;
+            uint32_t q = 0, avail = 0;
+            while (q < n) {
+                if (avail < q + 32u && avail < n) {
+                    avail = ctl->produced;
+                    if (avail < q + 32u && avail < n) {
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                }
+                if (q + 32u <= avail) {  // 32 occurrences: 8 ds_read_b128, in order
+                    const float4* src = reinterpret_cast<const float4*>(row + (q & (kHfRing - 1)));
+                    float4 v[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) v[k] = src[k];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        acc = acc + v[k].x;
+                        acc = acc + v[k].y;
+                        acc = acc + v[k].z;
+                        acc = acc + v[k].w;
+                    }
+                    q += 32u;
+                    ctl->consumed = q;  // every lane writes the same value
+                } else {  // the tail (avail == n)
+                    for (; q < n; ++q) acc = acc + row[q & (kHfRing - 1)];
+                }
+            }
+            if (f < d.dim) {
+                float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
+                                          c.key - pack.row_off[t]) + f;
+                store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+            }
+        } else {
+            const uint32_t E = info[g].y;  // real entries (padding follows)
+            const uint32_t* e = ent + c.e0;
+            const float* dcol = reinterpret_cast<const float*>(d.delta) + fc;
+            const uint64_t ld = (uint64_t)d.ld_delta;
+            uint32_t p = 0, cons = 0;
+            float x[2][kHfK];
+            uint32_t en[2][kHfK];
+            auto load = [&](int buf, uint32_t j0) {
+#pragma unroll
+                for (uint32_t k = 0; k < kHfK; ++k) {
+                    const uint32_t j = j0 + k;
+                    const uint32_t v = j < E ? e[j] : 0u;
+                    en[buf][k] = v;
+                    x[buf][k] = (v >> 24) ? dcol[(uint64_t)(v & 0xffffffu) * ld] : 0.0f;
+                }
+            };
+            load(0, 0u);
+            for (uint32_t j0 = 0; j0 < E; j0 += 2u * kHfK) {
+#pragma unroll
+                for (int half = 0; half < 2; ++half) {
+                    const uint32_t jb = j0 + (uint32_t)half * kHfK;
+                    if (jb >= E) break;
+                    load(half ^ 1, jb + kHfK);  // the next batch in flight
+#pragma unroll
+                    for (uint32_t k = 0; k < kHfK; ++k) {
+                        const uint32_t r = en[half][k] >> 24;
+                        if (r == 0u) continue;  // past E
+                        // the 16 slots from p may hold the previous lap's occurrences
+                        // [p + 16 - ring, ...): wait until they are consumed
+                        while (cons + kHfRing < p + 16u) {
+                            cons = ctl->consumed;
+                            if (cons + kHfRing < p + 16u) __builtin_amdgcn_s_sleep(1);
+                        }
+                        const uint32_t o = p & (kHfRing - 1);
+                        float* dst = row + o;
+                        const float v = x[half][k];
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) dst[i] = v;
+                        if (o + r > kHfRing) {  // wrapped copies
+                            float* dst2 = dst - kHfRing;
+#pragma unroll
+                            for (int i = 0; i < 16; ++i) dst2[i] = v;
+                        }
+                        p += r;
+                        // LDS requests of a wave are performed in order: the copies land
+                        // before the consumer can read this `produced`
+                        ctl->produced = p;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// The chains of an update phase (early or regular), in their own launch on a side stream.
+// Workgroups [0, nhf) run helper-fed pairs (waves 0/1 and 2/3, one item each at a time,
+// from counters[kCntHfNext]); the others take plain items — each wave the next of the
+// cost-ordered list from counters[kCntNext], which starts past the helper-fed ones — so
+// the longest chains start first and a late workgroup takes whatever is left.  A chain
+// issues a dependent VALU op about every 4.4 cycles, i.e. it alone nearly fills its SIMD's
+// VALU, so two chains must not share a SIMD: the launch reserves more than half of a CU's
+// LDS (the HF rings; untouched by plain workgroups), so no other chain workgroup — of this
+// launch or the other chain launch — lands on the same CU, and the workgroup's 4 waves
+// take its 4 SIMDs.  Top priority: the co-resident chunk-pass / singles / index-phase
+// waves (memory bound) take the leftover issue slots.
 template <int MODE, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chains(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64, int plain) {
-    extern __shared__ uint32_t reserve[];
-    (void)reserve;
+    const uint2* __restrict__ info, const uint32_t* __restrict__ nocc,
+    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64, int plain,
+    uint32_t nhf) {
+    extern __shared__ float lds[];
     const int lane = threadIdx.x & 63;
-    const uint32_t items = counters[kCntM] * (uint32_t)ns;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     __builtin_amdgcn_s_setprio(3);
-    for (;;) {
-        uint32_t it = 0;
-        if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
-        it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
-        if (it >= items) break;
-        sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it,
-                                 plain != 0);
+    if (blockIdx.x < nhf) {
+        HfCtl* ctl = reinterpret_cast<HfCtl*>(lds + 2 * 64 * kHfRow);
+        if (threadIdx.x < 2) ctl[threadIdx.x] = HfCtl{0u, 0u, 0u, 0u};
+        __syncthreads();
+        const int pair = wave >> 1;
+        hf_pair<MODE, NT>(pack, ntables, counters, chains, order, info, nocc, ent, ns, eta32,
+                          eta64, lds + pair * 64 * kHfRow, ctl + pair, (wave & 1) == 0);
+    } else {
+        const uint32_t items = counters[kCntM] * (uint32_t)ns;
+        for (;;) {
+            uint32_t it = 0;
+            if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
+            it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
+            if (it >= items) break;
+            sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it,
+                                     plain != 0);
+        }
     }
     __builtin_amdgcn_s_setprio(0);
 }
@@ -1919,7 +2112,7 @@ struct UpdateWs {
     // early chains (EcList): per (column, block) stats and entry offsets, per EC column the
     // padded entry count, (S, entries), descriptor and cost order, their entries, and a
     // counter block (kCntM = EC columns) for the chain role
-    uint32_t *ec_stats, *ec_boff, *ec_cnt, *ec_order, *ec_ent, *ec_counters;
+    uint32_t *ec_stats, *ec_boff, *ec_cnt, *ec_order, *ec_ent, *ec_counters, *ec_nocc;
     uint2* ec_info;
     ChainCol* ec_chains;
     int64_t bytes;
@@ -1987,6 +2180,7 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
         w.ec_boff = (uint32_t*)take(4 * recs);
         w.ec_cnt = (uint32_t*)take(4 * M);
         w.ec_order = (uint32_t*)take(4 * M);
+        w.ec_nocc = (uint32_t*)take(4 * M);
         w.ec_info = (uint2*)take(8 * M);
         w.ec_chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * M);
         w.ec_counters = (uint32_t*)take(4 * kCntSlots);
@@ -2180,6 +2374,12 @@ inline bool sgd_chunks_occ5() {
     return v;
 }
 
+inline unsigned env_uint(const char* name, unsigned dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? (unsigned)v : dflt;
+}
+
 // The chains of an exact update phase: the side stream of the early chains (null: none)
 // and their column count, the side stream of the regular chains (forked from the caller's
 // stream after the index phase).
@@ -2192,19 +2392,34 @@ struct ChainRun {
 // k_sgd_chains on stream `s`: zero the item counter, at most `nb` workgroups.
 template <int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
-                  const uint32_t* order, const uint32_t* ent, int ns, float eta32, double eta64,
+                  const uint32_t* order, const uint2* info, const uint32_t* nocc,
+                  const uint32_t* ent, int ns, float eta32, double eta64, unsigned nhf,
                   unsigned nb, hipStream_t s) {
     static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++
         const char* e = getenv("ET_CHAIN_ASM");
         return e && atoi(e) == 0 ? 1 : 0;
     }();
+    // experiments: ET_CHAIN_LDS = KiB reserved per chain workgroup (160: a whole CU)
+    static const uint32_t lds = [] {
+        const char* e = getenv("ET_CHAIN_LDS");
+        const int kb = e ? atoi(e) : 0;
+        return kb > 0 && kb <= 160 ? (uint32_t)kb * 1024u : kChainReserveLds;
+    }();
     static const hipError_t attr = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&k_sgd_chains<MODE, NT>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     ET_HIP_CHECK(attr);
-    ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
-    hipLaunchKernelGGL((k_sgd_chains<MODE, NT>), dim3(nb), dim3(256), kChainReserveLds, s, pack,
-                       ntables, counters, chains, order, ent, ns, eta32, eta64, plain);
+    // plain items start past the helper-fed ones (at 0 when no workgroup is helper-fed);
+    // the helper-fed counter at 0
+    if (nhf > 0)
+        ET_HIP_CHECK(hipMemcpyAsync(counters + kCntNext, counters + kCntHfItems, 4,
+                                    hipMemcpyDeviceToDevice, s));
+    else
+        ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
+    ET_HIP_CHECK(hipMemsetAsync(counters + kCntHfNext, 0, 4, s));
+    hipLaunchKernelGGL((k_sgd_chains<MODE, NT>), dim3(nhf + nb), dim3(256), lds, s, pack,
+                       ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64, plain,
+                       nhf);
     ET_LAUNCH_CHECK("k_sgd_chains");
     return ET_OK;
 }
@@ -2219,16 +2434,23 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                      const VecGroups& vg, bool any_generic, hipStream_t s, unsigned grid,
                      ChainRun cr) {
     const int ns = (pdim + 63) / 64;
+    // experiments: ET_EC_WG / ET_CHAIN_WG cap the early / regular chain workgroups
+    static const unsigned ec_wg = env_uint("ET_EC_WG", 256u), reg_wg = env_uint("ET_CHAIN_WG", 256u);
     int rc;
     if (cr.ec_side) {
         const int64_t items = (int64_t)cr.ec_ncols * ns;
-        const unsigned eb = (unsigned)(cdiv64(items, 4) < 256 ? cdiv64(items, 4) : 256);
+        const unsigned eb = (unsigned)(cdiv64(items, 4) < ec_wg ? cdiv64(items, 4) : ec_wg);
+        // helper-fed pairs: experimental (ET_HF_WG = workgroups + 1; their helper is
+        // latency-bound as written), off by default
+        static const unsigned hf_wg = env_uint("ET_HF_WG", 1u) - 1u;
         rc = launch_chains<MODE, NT>(pack, ntables, w.ec_counters, w.ec_chains, w.ec_order,
-                                     w.ec_ent, ns, eta32, eta64, eb, cr.ec_side);
+                                     w.ec_info, w.ec_nocc, w.ec_ent, ns, eta32, eta64, hf_wg, eb,
+                                     cr.ec_side);
         if (rc != ET_OK) return rc;
     }
-    rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order, w.chain_ent,
-                                 ns, eta32, eta64, 256u, cr.side);
+    rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
+                                 w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u, reg_wg,
+                                 cr.side);
     if (rc != ET_OK) return rc;
 #define ET_SGD_EXACT(DD)                                                                       \
     case DD:                                                                                   \
@@ -2458,6 +2680,18 @@ inline EcList ec_list(const et_update_desc* descs, int ntables, int64_t* occ) {
     return ec;
 }
 
+// Exact Float32 mode: columns of more occurrences than this are serial chains
+// (k_sgd_chains), the rest single chunks of the chunk pass (ET_EXACT_CHUNK, experiments).
+constexpr uint32_t kExactChunk = ET_SGD_CHUNK;
+inline uint32_t exact_chunk() {
+    static const uint32_t v = [] {
+        const char* e = getenv("ET_EXACT_CHUNK");
+        const int x = e ? atoi(e) : 0;
+        return x >= (int)ET_SGD_CHUNK ? (uint32_t)x : kExactChunk;
+    }();
+    return v;
+}
+
 // ET_EC=0 plans every chain from the sorted pairs (experiments).
 inline bool ec_enabled() {
     static const bool v = [] {
@@ -2530,15 +2764,15 @@ struct SideFork {
 
 // The early-chain plan (k_ec_count -> k_ec_plan -> k_ec_emit) on stream `s`.
 inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chunk,
-                          const UpdateWs& w, hipStream_t s) {
+                          const UpdateWs& w, int ns, hipStream_t s) {
     const uint32_t M = ec.col0[ec.n];
     ET_HIP_CHECK(hipMemsetAsync(w.ec_counters, 0, 4 * kCntSlots, s));
     hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_stats);
     hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
-                       w.ec_stats, w.ec_boff, w.ec_cnt, w.ec_info, w.ec_chains, w.ec_ent,
-                       w.ec_counters);
-    hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.ec_info, w.ec_order,
-                       w.ec_counters);
+                       w.ec_stats, w.ec_boff, w.ec_cnt, w.ec_nocc, w.ec_info, w.ec_chains,
+                       w.ec_ent, w.ec_counters);
+    hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.ec_info, w.ec_nocc, ns,
+                       w.ec_order, w.ec_counters);
     hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_boff,
                        w.ec_info, w.ec_ent);
     ET_LAUNCH_CHECK("k_ec_emit");
@@ -2595,8 +2829,11 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         if (descs[t].batch >= (1 << 24) || descs[t].ld_delta >= (1 << 22) ||
             (uint64_t)descs[t].batch * (uint64_t)descs[t].ld_delta >= (1ull << 30))
             chain = false;
-    const uint32_t chunk =
-        exact && !chain ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff) : et::kChunk;
+    // exact chain mode: a column of at most kExactChunk occurrences is one chunk of the
+    // chunk pass (a lane group's serial sum over full 512-byte rows), a longer one a chain
+    const uint32_t chunk = exact && !chain ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff)
+                           : chain          ? et::exact_chunk()
+                                            : et::kChunk;
     int nhot;
     int64_t hb, hbytes;
     uint64_t soff[ET_MAX_TABLES_PER_LAUNCH];
@@ -2668,7 +2905,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         ec_side = fork.fork(0);
         if (!ec_side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
         if (!apply_only) {
-            rc = et::launch_ec_plan(pack, ec, chunk, w, ec_side);
+            rc = et::launch_ec_plan(pack, ec, chunk, w, (pdim + 63) / 64, ec_side);
             if (rc != ET_OK) return rc;
         }
     }
