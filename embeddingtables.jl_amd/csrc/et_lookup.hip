@@ -1,4 +1,4 @@
-// et_lookup.hip — forward gather kernels for gfx950 (included by embtab.hip).
+// et_lookup.hip — forward gather kernels for gfx950.
 //
 // Replaces the reference's CPU kernels (darchr/EmbeddingTables.jl):
 //   lookup_generic! / lookup_static!        src/lookup.jl:51-182
@@ -498,14 +498,43 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
     }
 }
 
+#ifdef ET_WG_TIMELINE
+// Profiling build only (tools/wg_timeline.sh; never in the library the package loads):
+// every workgroup of the striped launch records its start / end on the 100 MHz
+// constant clock, its table, XCC and hardware slot, read back by et_debug_timeline.
+constexpr uint32_t kTlCap = 1u << 17;
+__device__ uint4 g_tl[kTlCap][2];
+#endif
+
 template <typename T, typename A, int D, int U, bool NT, bool NTI = false, bool SG = false>
 __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, StripeMap sm,
                                                             int ntables, int64_t batch,
                                                             T* __restrict__ dst, int64_t ld_dst,
                                                             int rounds, int64_t stripe_chunks,
                                                             int64_t nchunks) {
+#ifdef ET_WG_TIMELINE
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     striped_body<T, A, D, U, NT, NTI, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
                                           stripe_chunks, nchunks);
+#ifdef ET_WG_TIMELINE
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < kTlCap) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        uint32_t xcc, hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        const int x = blockIdx.x % kXcds;
+        const int64_t slot = blockIdx.x / kXcds;
+        const int64_t j = slot / ntables;
+        const uint32_t e = sm.entry[x][slot % ntables];
+        const int64_t chunk = (int64_t)(e >> 8) * stripe_chunks + j;
+        const uint32_t t = j >= stripe_chunks || chunk >= nchunks ? 0xffu : (e & 0xffu);
+        g_tl[blockIdx.x][0] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1,
+                                         (uint32_t)(t1 >> 32));
+        g_tl[blockIdx.x][1] = make_uint4(t, xcc, hw, gridDim.x);
+    }
+#endif
 }
 
 // The same kernel held to 64 VGPRs (8 waves per SIMD instead of 7): ET_W8=1 experiment.
@@ -1175,3 +1204,15 @@ extern "C" int et_maplookup_prealloc_to(int dtype, int dst_dtype, const et_looku
 }
 
 ET_OOB_READER(lookup)
+
+#ifdef ET_WG_TIMELINE
+// Profiling build only: copies the striped launch's workgroup records (2 x uint4 each)
+// to host memory; returns the number copied.
+extern "C" int et_debug_timeline(void* host, int64_t cap) {
+    const int64_t n = cap < (int64_t)et::kTlCap ? cap : (int64_t)et::kTlCap;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(et::g_tl), (size_t)n * 32, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return (int)n;
+}
+#endif

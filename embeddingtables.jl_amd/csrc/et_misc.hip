@@ -1,5 +1,5 @@
 // et_misc.hip — ABI housekeeping, synthetic-data fills and the multi-GPU concat
-// assembly (included by embtab.hip).
+// assembly (its own translation unit).
 #include "et_common.h"
 
 namespace et {

@@ -1,5 +1,5 @@
 // et_sort.hip — device-wide exclusive scan and stable LSD radix sort of
-// (uint32 key, uint32 value) pairs for gfx950 (included by embtab.hip).
+// (uint32 key, uint32 value) pairs for gfx950 (included by et_update.hip).
 //
 // These build the GPU equivalent of the reference's Indexer (src/utils.jl:88-314):
 // sorting occurrences by table column with a STABLE sort keeps each column's
