@@ -438,10 +438,15 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
     occ = batch * POOL * len(tables)
     upd_bytes = occ * 8 + batch * len(tables) * DIM * 4 + 2 * U * DIM * 4
     hot = max(int(torch.bincount(i.view(-1)).max()) for i in idx)
+    # the step as a host would run it: whichever of the two orderings is faster (in exact
+    # mode the early chains start with the update call, so the serial order usually wins)
+    best_ms = min(step_ms, overlap_ms)
     return {"workload": "26 Criteo tables x 128 fp32, Zipf(1.05) pool-20 indices, B=65536: "
                         "Preallocation forward + fused Descent(0.1) update of every table",
-            "lookups_per_s": occ / (overlap_ms * 1e-3), "step_ms": overlap_ms,
-            "step_note": "index phase of update! on a second stream beside the forward",
+            "lookups_per_s": occ / (best_ms * 1e-3), "step_ms": best_ms,
+            "step_order": "serial" if step_ms <= overlap_ms else "overlap",
+            "step_ms_overlap": overlap_ms,
+            "step_note": "overlap: index phase of update! on a second stream beside the forward",
             "step_ms_serial": step_ms, "lookups_per_s_serial": occ / (step_ms * 1e-3),
             "forward_ms": fwd_ms, "update_ms": upd_ms,
             "update_mode": "exact" if et.update.EXACT_DEFAULT else "split",

@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (loads torch's HIP runtime first, so the library shares it)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libembtab_hip.so")
+# ET_LIBRARY: an alternative build of the same library (the profiling builds under tools/)
+LIB_PATH = os.environ.get("ET_LIBRARY") or os.path.join(_HERE, "libembtab_hip.so")
 
 ET_OK = 0
 ET_F32, ET_F16, ET_F64, ET_I32, ET_I64, ET_BF16 = 0, 1, 2, 3, 4, 5

@@ -19,12 +19,11 @@ sys.path.insert(0, os.path.join(REPO, "embeddingtables.jl_amd"))
 
 
 def main():
+    os.environ["ET_LIBRARY"] = os.path.join(REPO, "tools", "tl", "libembtab_hip.so")
     import torch
 
-    from embtab import _lib
-
-    _lib.LIB_PATH = os.path.join(REPO, "tools", "tl", "libembtab_hip.so")
     import bench
+    from embtab import _lib
     import embtab as et
 
     L = _lib.load()
