@@ -2434,8 +2434,12 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                      const VecGroups& vg, bool any_generic, hipStream_t s, unsigned grid,
                      ChainRun cr) {
     const int ns = (pdim + 63) / 64;
-    // experiments: ET_EC_WG / ET_CHAIN_WG cap the early / regular chain workgroups
-    static const unsigned ec_wg = env_uint("ET_EC_WG", 256u), reg_wg = env_uint("ET_CHAIN_WG", 256u);
+    // chain workgroups (one CU each): 32 early, 128 regular, so the regular chains find
+    // free CUs when the index phase releases them instead of waiting for early-chain
+    // workgroups (config 4, one box, twice: 256/256 4.62-4.63 ms, 32/128 4.19-4.27,
+    // 16/96 4.25-4.29, 64/192 4.42-4.44; profiles/r03/b/ab_exact_knobs.txt).
+    // ET_EC_WG / ET_CHAIN_WG override (experiments).
+    static const unsigned ec_wg = env_uint("ET_EC_WG", 32u), reg_wg = env_uint("ET_CHAIN_WG", 128u);
     int rc;
     if (cr.ec_side) {
         const int64_t items = (int64_t)cr.ec_ncols * ns;
