@@ -1743,20 +1743,135 @@ __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
     }
 }
 
-// Update phase, chain role: one (column, 64-feature slice) item of the cost-ordered list:
-// the serial sum of the slice's gradient columns and the update.
+// S = 1 chains (every entry one add: the big tables' hot columns, whose runs are single
+// occurrences) are bound by memory latency, not issue: a wave keeps at most 63 vector
+// loads in flight (vmcnt), i.e. 63 entries of one 64-feature slice, and a random 256-byte
+// gradient row takes ~1-2 us to arrive under the update's load.  The quad walk carries
+// FOUR entries per load: the wave covers 16 features, its four 16-lane rows load the
+// 16-feature slices of four consecutive entries, and the serial sum takes them into row 0
+// in order (permlane16 / permlane32 swaps move rows 1-3 down), so 32 loads in flight are
+// 128 entries.  The 64-entry chunk is loaded permuted (lane 16r + k holds entry 4k + r),
+// so DPP row_newbcast:k hands row r entry 4k + r.  Same adds in the same order as the
+// 64-feature loop (bit-identical); rows 1-3 add garbage that is never stored.
+constexpr int kQuadRing = 32;   // quads (4 entries each) of gradient loads in flight
+constexpr int kQuadItems = 4;   // work items per (column, 64-feature slice): 16-feature quarters
+constexpr int kQuadMinGroups = 256;  // quad walk for S = 1 chains of >= 16 K entries
+
+template <int K>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + K, 0xf, 0xf, false);
+}
+
+template <int J, int N>
+__device__ __forceinline__ void quad_trip(float (&x)[kQuadRing], float& acc, uint32_t cnext0,
+                                          uint32_t cnext1, __amdgpu_buffer_rsrc_t rx,
+                                          uint32_t ld4, uint32_t lane4) {
+    if constexpr (J < N) {
+        const uint32_t v = __float_as_uint(x[J]);
+        acc = acc + x[J];                                            // entry 4q
+        const auto s32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        const auto s16 = __builtin_amdgcn_permlane16_swap(s32[0], s32[0], false, false);
+        acc = acc + __uint_as_float(s16[1]);                         // entry 4q + 1
+        const uint32_t z = s32[1];                                   // rows: 4q+2, 4q+3, ..
+        acc = acc + __uint_as_float(z);                              // entry 4q + 2
+        const auto t16 = __builtin_amdgcn_permlane16_swap(z, z, false, false);
+        acc = acc + __uint_as_float(t16[1]);                         // entry 4q + 3
+        // quad q + kQuadRing into x[J] (its bag from the chunk two chunks on)
+        const uint32_t bag = row_bcast<J & 15>(J < 16 ? cnext0 : cnext1);
+        x[J] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rx, (int)(__umul24(bag, ld4) + lane4), 0, 0));
+        quad_trip<J + 1, N>(x, acc, cnext0, cnext1, rx, ld4, lane4);
+    }
+}
+
+template <int J, int N>
+__device__ __forceinline__ void quad_prologue(float (&x)[kQuadRing], uint32_t c0, uint32_t c1,
+                                              __amdgpu_buffer_rsrc_t rx, uint32_t ld4,
+                                              uint32_t lane4) {
+    if constexpr (J < N) {
+        const uint32_t bag = row_bcast<J & 15>(J < 16 ? c0 : c1);
+        x[J] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rx, (int)(__umul24(bag, ld4) + lane4), 0, 0));
+        quad_prologue<J + 1, N>(x, c0, c1, rx, ld4, lane4);
+    }
+}
+
+// The serial sum of one S = 1 chain over 16 features (row 0 of the result).  ent: the
+// chain's entries (ngr x 64, then >= kChainPad padding entries that address bag `batch`,
+// past the gradient's range: they load +0); P: entries readable (range of the entry loads,
+// past it they read 0).  Trips of 2 chunks (32 quads); the last trip's adds reach at most
+// 64 entries past ngr x 64, inside the padding.
+__device__ __forceinline__ float chain_walk_quad(const uint32_t* ent, uint32_t ngr, uint32_t P,
+                                                 const float* delta, uint32_t range,
+                                                 uint32_t lane4, uint32_t ld4) {
+    static_assert(kChainPad >= 64 && kQuadRing == 32, "quad walk layout");
+    const int lane = threadIdx.x & 63;
+    const uint32_t poff = 4u * (4u * (uint32_t)(lane & 15) + (uint32_t)(lane >> 4));
+    const __amdgpu_buffer_rsrc_t rx =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(delta), 0, (int)range, 0x00020000);
+    const __amdgpu_buffer_rsrc_t re =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(ent), 0, (int)(4u * P), 0x00020000);
+    auto chunk = [&](uint32_t c) { return __builtin_amdgcn_raw_buffer_load_b32(re, (int)(c * 256u + poff), 0, 0); };
+    const uint32_t c0 = chunk(0), c1 = chunk(1);
+    uint32_t n0 = chunk(2), n1 = chunk(3);
+    float x[kQuadRing];
+    quad_prologue<0, kQuadRing>(x, c0, c1, rx, ld4, lane4);  // quads 0..31 (chunks 0, 1)
+    float acc = 0.0f;
+    const uint32_t trips = (ngr + 1u) / 2u;
+    for (uint32_t t = 0; t < trips; ++t) {
+        const uint32_t m0 = chunk(2u * t + 4u), m1 = chunk(2u * t + 5u);
+        quad_trip<0, kQuadRing>(x, acc, n0, n1, rx, ld4, lane4);
+        n0 = m0;
+        n1 = m1;
+    }
+    return acc;
+}
+
+// Update phase, chain role: one (column, 64-feature slice, quarter) item of the cost-
+// ordered list: the serial sum of the slice's gradient columns and the update.  An S = 1
+// chain takes its four quarters as four items (the quad walk, 16 features each); any other
+// chain takes the whole slice in quarter 0 (the other quarters return at once).
 template <int MODE, bool NT>
 __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntables,
                                                const ChainCol* __restrict__ chains,
                                                const uint32_t* __restrict__ order,
                                                const uint32_t* __restrict__ ent, int ns,
-                                               float eta32, double eta64, uint32_t it,
-                                               bool plain) {
+                                               float eta32, double eta64, uint32_t it4,
+                                               int how) {
     const int lane = threadIdx.x & 63;
+    const bool plain = (how & 1) != 0;  // debug: the plain C++ loop for every chain
+    const uint32_t quarter = it4 % (uint32_t)kQuadItems, it = it4 / (uint32_t)kQuadItems;
     const ChainCol c = chains[order[it / (uint32_t)ns]];
     if (c.S == 0u) return;
+    // the quad walk for long S = 1 chains only (how >> 2 = the minimum in 64-entry groups):
+    // it spends 4 waves where the 64-feature loop spends one, so short chains, which are
+    // throughput- rather than latency-bound, keep the loop; how & 2 turns it off
+    const bool quad = c.S == 1u && (how & 3) == 0 && c.ngr >= ((uint32_t)how >> 2);
+    if (!quad && quarter != 0u) return;
     const int t = table_of_key(pack, ntables, c.key);
     const et_update_desc& d = pack.d[t];
+    if (quad) {
+        const int f0 = (int)(it % (uint32_t)ns) * 64 + (int)quarter * 16;
+        if (f0 >= d.dim) return;  // uniform
+        const int f = f0 + (lane & 15);
+        const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
+        const uint32_t ld = (uint32_t)d.ld_delta;
+        const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
+        const float* delta = reinterpret_cast<const float*>(
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
+        const uint64_t eb = reinterpret_cast<uint64_t>(ent + c.e0);
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)eb) |
+            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(eb >> 32)) << 32);
+        const float acc = chain_walk_quad(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
+                                          (uint32_t)d.batch * ld * 4u, 4u * fc, 4u * ld);
+        if (lane < 16 && f < d.dim) {
+            float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
+            store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+        }
+        return;
+    }
     const int f = (int)(it % (uint32_t)ns) * 64 + lane;
     if ((int)(it % (uint32_t)ns) * 64 >= d.dim) return;  // uniform
     const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
@@ -1981,14 +2096,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         hf_pair<MODE, NT>(pack, ntables, counters, chains, order, info, nocc, ent, ns, eta32,
                           eta64, lds + pair * 64 * kHfRow, ctl + pair, (wave & 1) == 0);
     } else {
-        const uint32_t items = counters[kCntM] * (uint32_t)ns;
+        const uint32_t items = counters[kCntM] * (uint32_t)ns * (uint32_t)kQuadItems;
         for (;;) {
             uint32_t it = 0;
             if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
             it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
             if (it >= items) break;
             sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it,
-                                     plain != 0);
+                                     plain);
         }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -2395,9 +2510,13 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
                   const uint32_t* order, const uint2* info, const uint32_t* nocc,
                   const uint32_t* ent, int ns, float eta32, double eta64, unsigned nhf,
                   unsigned nb, hipStream_t s) {
-    static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++
+    static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++;
+        // experiments: ET_CHAIN_QUAD=0 walks S = 1 chains with the 64-feature asm loop
         const char* e = getenv("ET_CHAIN_ASM");
-        return e && atoi(e) == 0 ? 1 : 0;
+        const char* q = getenv("ET_CHAIN_QUAD");
+        const char* m = getenv("ET_QUAD_MIN");  // experiments: quad-walk threshold
+        const int qmin = m ? atoi(m) : kQuadMinGroups;
+        return (e && atoi(e) == 0 ? 1 : 0) | (q && atoi(q) == 0 ? 2 : 0) | (qmin << 2);
     }();
     // experiments: ET_CHAIN_LDS = KiB reserved per chain workgroup (160: a whole CU)
     static const uint32_t lds = [] {
@@ -2444,9 +2563,10 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     if (cr.ec_side) {
         const int64_t items = (int64_t)cr.ec_ncols * ns;
         const unsigned eb = (unsigned)(cdiv64(items, 4) < ec_wg ? cdiv64(items, 4) : ec_wg);
-        // helper-fed pairs: experimental (ET_HF_WG = workgroups + 1; their helper is
-        // latency-bound as written), off by default
-        static const unsigned hf_wg = env_uint("ET_HF_WG", 1u) - 1u;
+        // helper-fed pairs (k_sgd_chains' first nhf workgroups): kept for experiments but
+        // off — their helper was latency-bound, and the plain items are numbered per
+        // quarter (kQuadItems) since the quad walk
+        const unsigned hf_wg = 0u;
         rc = launch_chains<MODE, NT>(pack, ntables, w.ec_counters, w.ec_chains, w.ec_order,
                                      w.ec_info, w.ec_nocc, w.ec_ent, ns, eta32, eta64, hf_wg, eb,
                                      cr.ec_side);
