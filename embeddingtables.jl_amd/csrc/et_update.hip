@@ -1755,7 +1755,7 @@ __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
 // 64-feature loop (bit-identical); rows 1-3 add garbage that is never stored.
 constexpr int kQuadRing = 32;   // quads (4 entries each) of gradient loads in flight
 constexpr int kQuadItems = 4;   // work items per (column, 64-feature slice): 16-feature quarters
-constexpr int kQuadMinGroups = 256;  // quad walk for S = 1 chains of >= 16 K entries
+constexpr int kQuadMinGroups = 1024;  // quad walk for S = 1 chains of >= 64 K entries
 
 template <int K>
 __device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
