@@ -2109,6 +2109,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     __builtin_amdgcn_s_setprio(0);
 }
 
+// The same chain loop (plain items only) on SIMDs of its own: the kernel writes a255, so
+// it is allocated the whole accumulation-register file besides its VGPRs and no other
+// wave — of the chunk pass, the singles, the index phase — can be resident on its SIMDs
+// while it runs; the chain waves then issue at the SIMD's own rate instead of sharing it
+// (ET_CHAIN_EXCL: bit 0 the early chains, bit 1 the regular ones).
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_chains_x(
+    UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
+    const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
+    const uint2* __restrict__ info, const uint32_t* __restrict__ nocc,
+    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64, int plain,
+    uint32_t nhf) {
+    asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+    const int lane = threadIdx.x & 63;
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t items = counters[kCntM] * (uint32_t)ns * (uint32_t)kQuadItems;
+    for (;;) {
+        uint32_t it = 0;
+        if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
+        it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
+        if (it >= items) break;
+        sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it, plain);
+    }
+    __builtin_amdgcn_s_setprio(0);
+}
+
 // The rest of the update phase of an exact Float32 call in one launch: blocks [0, nch)
 // the chunk pass over single-chunk columns of this capacity group, the rest the
 // single-occurrence columns (the chains run in k_sgd_chains on the side streams).
@@ -2509,7 +2535,7 @@ template <int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
                   const uint32_t* order, const uint2* info, const uint32_t* nocc,
                   const uint32_t* ent, int ns, float eta32, double eta64, unsigned nhf,
-                  unsigned nb, hipStream_t s) {
+                  unsigned nb, hipStream_t s, bool excl = false) {
     static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++;
         // experiments: ET_CHAIN_QUAD=0 walks S = 1 chains with the 64-feature asm loop
         const char* e = getenv("ET_CHAIN_ASM");
@@ -2528,6 +2554,10 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         reinterpret_cast<const void*>(&k_sgd_chains<MODE, NT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     ET_HIP_CHECK(attr);
+    static const hipError_t attr_x = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&k_sgd_chains_x<MODE, NT>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    ET_HIP_CHECK(attr_x);
     // plain items start past the helper-fed ones (at 0 when no workgroup is helper-fed);
     // the helper-fed counter at 0
     if (nhf > 0)
@@ -2536,6 +2566,13 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
     else
         ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
     ET_HIP_CHECK(hipMemsetAsync(counters + kCntHfNext, 0, 4, s));
+    if (excl && nhf == 0) {
+        hipLaunchKernelGGL((k_sgd_chains_x<MODE, NT>), dim3(nb), dim3(256), lds, s, pack,
+                           ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64,
+                           plain, 0u);
+        ET_LAUNCH_CHECK("k_sgd_chains_x");
+        return ET_OK;
+    }
     hipLaunchKernelGGL((k_sgd_chains<MODE, NT>), dim3(nhf + nb), dim3(256), lds, s, pack,
                        ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64, plain,
                        nhf);
@@ -2559,6 +2596,14 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     // 16/96 4.25-4.29, 64/192 4.42-4.44; profiles/r03/b/ab_exact_knobs.txt).
     // ET_EC_WG / ET_CHAIN_WG override (experiments).
     static const unsigned ec_wg = env_uint("ET_EC_WG", 32u), reg_wg = env_uint("ET_CHAIN_WG", 128u);
+    // chain launches on SIMDs of their own (k_sgd_chains_x): bit 0 early, bit 1 regular.
+    // The early chains only (config 4, A/B twice on one box: none 4.02-4.11 ms, early
+    // 4.015-4.017, regular 4.33-4.34, both 4.35; profiles/r03/e/ab_chain_excl.txt): the
+    // regular chains run beside the chunk pass, which needs those SIMDs more.
+    static const unsigned excl = [] {
+        const char* e = getenv("ET_CHAIN_EXCL");
+        return e ? (unsigned)atoi(e) & 3u : 1u;
+    }();
     int rc;
     if (cr.ec_side) {
         const int64_t items = (int64_t)cr.ec_ncols * ns;
@@ -2569,12 +2614,12 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         const unsigned hf_wg = 0u;
         rc = launch_chains<MODE, NT>(pack, ntables, w.ec_counters, w.ec_chains, w.ec_order,
                                      w.ec_info, w.ec_nocc, w.ec_ent, ns, eta32, eta64, hf_wg, eb,
-                                     cr.ec_side);
+                                     cr.ec_side, (excl & 1u) != 0);
         if (rc != ET_OK) return rc;
     }
     rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
                                  w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u, reg_wg,
-                                 cr.side);
+                                 cr.side, (excl & 2u) != 0);
     if (rc != ET_OK) return rc;
 #define ET_SGD_EXACT(DD)                                                                       \
     case DD:                                                                                   \
