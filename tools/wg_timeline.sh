@@ -1,7 +1,8 @@
 #!/bin/bash
 # Profiling build of the library with per-workgroup timestamps in the striped lookup
 # (-DET_WG_TIMELINE): tools/tl/libembtab_hip.so.  The package's own library is untouched.
-# Build here (CPU), run tools/wg_timeline.py on the GPU box.
+# Build here (CPU), run tools/wg_timeline.py on the GPU box (tools/tl is listed in
+# .gpurunignore so the 12 MB build does not travel with every call: drop that line first).
 set -e
 cd "$(dirname "$0")/.."
 python3 -c "import __graft_entry__ as g; g.build_hip()"
