@@ -413,8 +413,8 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
     overlap_ms = _timed(step_overlap, steps, warmup, stream)
     # the other update mode, and how far the split mode lies from the exact (reference-
     # order, src/sparseupdate.jl:110-127) result: both from the same tables, every element
-    other = not et.update.EXACT_DEFAULT
-    other_ms = _timed(lambda: et.update_(opt, tables, grads, indexers, exact=other), steps,
+    # (the default resolves to the exact mode for these Float32 tables: ET_FLAG_EXACT_IF_FAST)
+    other_ms = _timed(lambda: et.update_(opt, tables, grads, indexers, exact=False), steps,
                       warmup, stream)
     w0 = [A.data.clone() for A in tables]
     res = {}
@@ -432,8 +432,7 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
         differ += int((sp != e).sum())
     del res, w0
     torch.cuda.empty_cache()
-    exact_ms = upd_ms if et.update.EXACT_DEFAULT else other_ms
-    split_ms = other_ms if et.update.EXACT_DEFAULT else upd_ms
+    exact_ms, split_ms = upd_ms, other_ms
     U = sum(int(torch.unique(i).numel()) for i in idx)
     occ = batch * POOL * len(tables)
     upd_bytes = occ * 8 + batch * len(tables) * DIM * 4 + 2 * U * DIM * 4
@@ -449,7 +448,7 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
             "step_note": "overlap: index phase of update! on a second stream beside the forward",
             "step_ms_serial": step_ms, "lookups_per_s_serial": occ / (step_ms * 1e-3),
             "forward_ms": fwd_ms, "update_ms": upd_ms,
-            "update_mode": "exact" if et.update.EXACT_DEFAULT else "split",
+            "update_mode": "exact",
             "update_exact_ms": exact_ms, "update_split_ms": split_ms,
             "exact_over_split": exact_ms / split_ms,
             # the split mode (long columns as ordered partial sums) against the exact one,

@@ -87,7 +87,16 @@ struct LoopGroup {
 struct LoopComm {
     LoopGroup* g;
     int rank;
+    bool exchange_failed = false;  // the last failure of this rank came from loop_exchange
 };
+
+// A rank that fails before it joins a collective never arrives: mark the group broken and
+// wake its peers, which then return an error at once instead of after the 120 s timeout.
+static void loop_abort(LoopComm* c) {
+    std::lock_guard<std::mutex> lk(c->g->mu);
+    c->g->broken = true;
+    c->g->cv.notify_all();
+}
 
 static std::mutex g_loop_mu;
 static std::set<const void*> g_loop_comms;  // handles made by et_comm_loopback
@@ -99,7 +108,14 @@ static LoopComm* as_loop(const void* comm) {
 
 // One loopback exchange: rank r sends send[p] (sbytes[p]) to every peer p and receives
 // recv[p] (rbytes[p]) from it.  Collective over the group's ranks; stream-ordered on st.
+static int loop_exchange_impl(LoopComm* c, LoopPost&& mine, hipStream_t st);
 static int loop_exchange(LoopComm* c, LoopPost&& mine, hipStream_t st) {
+    const int rc = loop_exchange_impl(c, std::move(mine), st);
+    c->exchange_failed = rc != ET_OK;
+    return rc;
+}
+
+static int loop_exchange_impl(LoopComm* c, LoopPost&& mine, hipStream_t st) {
     LoopGroup& g = *c->g;
     const int r = c->rank;
     hipError_t e = hipEventRecord(g.ready[r], st);
@@ -605,12 +621,44 @@ static int check_local(Sharded* s, const et_lookup_desc* local, int32_t nlocal) 
     return ET_OK;
 }
 
+// A loopback rank whose step fails outside a collective (argument checks, a lookup launch)
+// aborts its group, so its peers' pending collectives fail fast.
+static int loop_guard(Sharded* s, int rc) {
+    if (rc != ET_OK && s->loop && !s->loop->exchange_failed) et::loop_abort(s->loop);
+    return rc;
+}
+
+static int sharded_maplookup(Sharded* s, const et_lookup_desc* local, int32_t nlocal, void* dst,
+                             int64_t ld_dst, void* workspace, int64_t ws_bytes, uint32_t flags,
+                             void* stream);
+static int sharded_piece_grads(Sharded* s, const void* delta, int64_t ld_delta, void* recv,
+                               void* workspace, int64_t ws_bytes, void* stream);
+
 extern "C" int et_sharded_maplookup(void* handle, const et_lookup_desc* local, int32_t nlocal,
                                     void* dst, int64_t ld_dst, void* workspace, int64_t ws_bytes,
                                     uint32_t flags, void* stream) {
     et::clear_err();
     if (!handle) return et::fail(ET_ERR_ARG, "handle is NULL");
     Sharded* s = (Sharded*)handle;
+    if (s->loop) s->loop->exchange_failed = false;
+    return loop_guard(s, sharded_maplookup(s, local, nlocal, dst, ld_dst, workspace, ws_bytes,
+                                           flags, stream));
+}
+
+extern "C" int et_sharded_piece_grads(void* handle, const void* delta, int64_t ld_delta,
+                                      void* recv, void* workspace, int64_t ws_bytes,
+                                      void* stream) {
+    et::clear_err();
+    if (!handle) return et::fail(ET_ERR_ARG, "handle is NULL");
+    Sharded* s = (Sharded*)handle;
+    if (s->loop) s->loop->exchange_failed = false;
+    return loop_guard(s, sharded_piece_grads(s, delta, ld_delta, recv, workspace, ws_bytes,
+                                             stream));
+}
+
+static int sharded_maplookup(Sharded* s, const et_lookup_desc* local, int32_t nlocal, void* dst,
+                             int64_t ld_dst, void* workspace, int64_t ws_bytes, uint32_t flags,
+                             void* stream) {
     int rc = check_local(s, local, nlocal);
     if (rc != ET_OK) return rc;
     if (ld_dst < s->ld_dst) return et::fail(ET_ERR_ARG, "ld_dst %lld < plan's %lld", (long long)ld_dst, (long long)s->ld_dst);
@@ -670,12 +718,8 @@ extern "C" int et_sharded_maplookup(void* handle, const et_lookup_desc* local, i
     return ET_OK;
 }
 
-extern "C" int et_sharded_piece_grads(void* handle, const void* delta, int64_t ld_delta,
-                                      void* recv, void* workspace, int64_t ws_bytes,
-                                      void* stream) {
-    et::clear_err();
-    if (!handle) return et::fail(ET_ERR_ARG, "handle is NULL");
-    Sharded* s = (Sharded*)handle;
+static int sharded_piece_grads(Sharded* s, const void* delta, int64_t ld_delta, void* recv,
+                               void* workspace, int64_t ws_bytes, void* stream) {
     if (s->exchange != ET_EXCHANGE_ALLTOALL)
         return et::fail(ET_ERR_ARG, "all-gather layout: a piece's gradient is a column view of "
                                     "the replicated gradient (no exchange)");

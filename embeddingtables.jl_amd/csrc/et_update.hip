@@ -1491,7 +1491,10 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
             const uint32_t e = ent[c.e0 + i], r = e >> 24;
             const bool ok = ((uint64_t)(e & 0xffffffu) < lim || (r == 0u && (e & 0xffffffu) == lim)) &&
                             r <= c.S;
-            if (!ok) ent[c.e0 + i] = 0u;
+            // a bad entry becomes a padding entry (bag = batch: its range-checked load
+            // returns +0), so the debug pass reports the violation without adding
+            // gradient column 0 in its place (maskless S = 1 and quad walks add every entry)
+            if (!ok) ent[c.e0 + i] = chain_entry(0u, (uint32_t)lim);
             bad += ok ? 0u : 1u;
             real += (ok && r > 0u) ? 1u : 0u;
             pad_then_real += (ok && r > 0u && i >= info[m].y) ? 1u : 0u;
@@ -2988,16 +2991,19 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
     if (rc != ET_OK) return rc;
     if (n == 0) return ET_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const bool exact = (flags & ET_FLAG_EXACT_UPDATE) != 0;
+    const bool exact_forced = (flags & ET_FLAG_EXACT_UPDATE) != 0;
     // Exact Float32: columns longer than a chunk are summed as serial chains (k_chain_*,
     // k_sgd_exact), whose entries hold a 24-bit bag and whose loop addresses the gradient
     // by a 32-bit byte offset (bag * ld * 4 from 24-bit factors).  Other exact calls keep
     // every column in one chunk (a chunk spans a whole segment).
-    bool chain = exact && dtype == ET_F32;
+    bool chain = (exact_forced || (flags & ET_FLAG_EXACT_IF_FAST)) && dtype == ET_F32;
     for (int t = 0; t < ntables && chain; ++t)
         if (descs[t].batch >= (1 << 24) || descs[t].ld_delta >= (1 << 22) ||
             (uint64_t)descs[t].batch * (uint64_t)descs[t].ld_delta >= (1ull << 30))
             chain = false;
+    // ET_FLAG_EXACT_IF_FAST: exact only where the chains run (decided from the descriptors
+    // alone, so an INDEX_ONLY and its APPLY_ONLY call agree)
+    const bool exact = exact_forced || chain;
     // exact chain mode: a column of at most kExactChunk occurrences is one chunk of the
     // chunk pass (a lane group's serial sum over full 512-byte rows), a longer one a chain
     const uint32_t chunk = exact && !chain ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff)

@@ -19,6 +19,7 @@ ET_F32, ET_F16, ET_F64, ET_I32, ET_I64, ET_BF16 = 0, 1, 2, 3, 4, 5
 ET_FLAG_NONTEMPORAL = 1
 ET_FLAG_F16_FP32_ACC = 2
 ET_FLAG_EXACT_UPDATE = 4
+ET_FLAG_EXACT_IF_FAST = 256
 ET_FLAG_SGD_UNFUSED = 8
 ET_FLAG_SGD_F64_ALPHA = 16
 ET_FLAG_SGD_INDEX_ONLY = 32
@@ -26,7 +27,7 @@ ET_FLAG_SGD_APPLY_ONLY = 64
 ET_FLAG_SGD_HOT_PASS = 128
 ET_MAX_TABLES_PER_LAUNCH = 32
 ET_SGD_CHUNK = 256  # include/embtab.h: occurrences per chunk of the non-exact SGD
-ET_ABI_VERSION = 7
+ET_ABI_VERSION = 8
 ET_MAX_PEERS = 16
 ET_PLAN_TABLEWISE, ET_PLAN_FEATUREWISE = 0, 1
 ET_EXCHANGE_ALLGATHER, ET_EXCHANGE_ALLTOALL = 0, 1

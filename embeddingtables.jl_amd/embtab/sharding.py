@@ -206,6 +206,9 @@ class ShardedMapLookup:
         self._native = None
         auto = native is None
         if comm is not None:  # a caller-owned communicator (e.g. a loopback rank)
+            if exchange == "p2p":
+                raise ValueError("exchange='p2p' has no native step: comm= applies to the "
+                                 "'allgather' and 'alltoall' exchanges only")
             native, auto = True, False
         if auto:  # the C-ABI step whenever the ranks are real GPU processes
             native = (exchange != "p2p" and self.device.type == "cuda" and

@@ -25,6 +25,7 @@ const libhip = "libamdhip64.so"
 const ET_F32, ET_F16, ET_F64, ET_I32, ET_I64 = Cint(0), Cint(1), Cint(2), Cint(3), Cint(4)
 const ET_FLAG_NONTEMPORAL = UInt32(1)
 const ET_FLAG_EXACT_UPDATE = UInt32(4)      # every column summed serially (bit-identical)
+const ET_FLAG_EXACT_IF_FAST = UInt32(256)   # exact where the chain path runs (Float32), else split
 const ET_FLAG_SGD_UNFUSED = UInt32(8)
 const ET_FLAG_SGD_F64_ALPHA = UInt32(16)
 const ET_FLAG_SGD_INDEX_ONLY = UInt32(32)   # phase 1 of update!: index all (src/sparseupdate.jl:210-213)
@@ -334,16 +335,21 @@ function _sparse_sgd(::Type{T}, descs::Vector{UpdateDesc}, eta::Float64, flags::
 end
 
 # The exact update (ET_FLAG_EXACT_UPDATE, every column's gradient summed serially in the
-# reference's order) is the default; exact = false selects the split mode (long columns
-# summed as ordered partial sums: deterministic, not bit-identical).
-const EXACT = Ref(true)
+# reference's order) is the default wherever it has its fast serial-chain path: the default
+# `nothing` passes ET_FLAG_EXACT_IF_FAST (exact for Float32 tables, the split mode for
+# Float64 / Float16, whose exact mode sums a hot column in one wave); exact = true forces
+# it for every eltype, exact = false selects the split mode (long columns summed as
+# ordered partial sums: deterministic, not bit-identical).
+const EXACT = Ref{Union{Nothing,Bool}}(nothing)
+_exact_flag(exact) = exact === nothing ? ET_FLAG_EXACT_IF_FAST :
+                     exact ? ET_FLAG_EXACT_UPDATE : UInt32(0)
 
 function update!(opt::Flux.Descent, table::HipTable{S,T}, grad::SparseEmbeddingUpdate,
                  indexer = Indexer(), ::Val{Nontemporal} = Val(true),
-                 args...; exact::Bool = EXACT[]) where {S,T<:UpdateEltype,Nontemporal}
+                 args...; exact::Union{Nothing,Bool} = EXACT[]) where {S,T<:UpdateEltype,Nontemporal}
     flags = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
             (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED) |
-            (exact ? ET_FLAG_EXACT_UPDATE : UInt32(0))
+            _exact_flag(exact)
     # convert(eltype(table), opt.eta) happens inside the library
     _sparse_sgd(T, [_update_desc(table, grad)], Float64(opt.eta), flags)
     return nothing
@@ -417,9 +423,8 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  grads::AbstractVector{<:SparseEmbeddingUpdate},
                  indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
                  telemetry_cb = nothing, fill_host_indexers::Bool = false,
-                 exact::Bool = EXACT[], kw...) where {Nontemporal}
-    nt = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
-         (exact ? ET_FLAG_EXACT_UPDATE : UInt32(0))
+                 exact::Union{Nothing,Bool} = EXACT[], kw...) where {Nontemporal}
+    nt = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) | _exact_flag(exact)
     calls = []
     for fused in (true, false), T in (Float32, Float64, Float16)
         sel = [i for i in eachindex(tables) if _fused(tables[i]) == fused &&

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 7
+#define ET_ABI_VERSION 8
 
 /* Status codes. */
 #define ET_OK 0
@@ -88,6 +88,12 @@ extern "C" {
                                     bag-major over 1024-bag windows instead of by per-
                                     occurrence gathers (deterministic; EXPERIMENTAL, slower
                                     today — DESIGN.md §7) */
+#define ET_FLAG_EXACT_IF_FAST 256u /* sparse SGD (ABI v8): ET_FLAG_EXACT_UPDATE where the
+                                    exact mode has its fast serial-chain path (Float32 with
+                                    batch < 2^24, ld_delta < 2^22 and batch * ld_delta < 2^30
+                                    for every descriptor), the split mode otherwise (other
+                                    dtypes would sum a hot column in one wave per column);
+                                    the bindings' default.  Ignored with ET_FLAG_EXACT_UPDATE */
 
 /* Occurrences per chunk of the non-exact sparse SGD: a column with more occurrences than
  * this is summed as ordered partial sums of ET_SGD_CHUNK consecutive occurrences (so a

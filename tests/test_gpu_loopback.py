@@ -211,3 +211,46 @@ def test_config5_native_step_loopback_8_ranks(oracle, planner):
         ranks.close()
         del tabs, idx, base
         torch.cuda.empty_cache()
+
+
+def test_loopback_rank_failing_before_collective_aborts_group():
+    """A loopback rank whose step fails before its collective (here: a wrong descriptor
+    count, refused by the argument check) aborts the group, so its peer's pending
+    all-gather returns an error at once instead of after the 120 s rendezvous timeout
+    (et_shard.cpp loop_abort)."""
+    import time
+
+    world, B, k = 2, 257, 0
+    rng, hs, hidx, full, didx = _setup(5, DIMS, ROWS, B)
+    plan = ShardPlan.tablewise(DIMS, world, k)
+    ranks = Ranks(plan, world, B, "allgather", 1)
+    try:
+        outs = [torch.empty((B, plan.ld), dtype=torch.float32, device=DEV) for _ in range(world)]
+        tabs = [[piece_table(full[p.table], p) for p in plan.pieces[r]] for r in range(world)]
+        idxs = [[didx[p.table] for p in plan.pieces[r]] for r in range(world)]
+        assert len(tabs[1]) >= 2
+        errs = [None] * world
+
+        def body(r):
+            try:
+                if r == 1:  # one descriptor short: fails before joining the all-gather
+                    ranks.steps[r](tabs[r][:-1], idxs[r][:-1], outs[r])
+                else:
+                    ranks.steps[r](tabs[r], idxs[r], outs[r])
+            except _lib.EmbtabError as e:
+                errs[r] = e
+
+        t0 = time.monotonic()
+        th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=150)
+        elapsed = time.monotonic() - t0
+        assert not any(t.is_alive() for t in th), "a rank hung"
+        assert errs[1] is not None and "descriptors given" in str(errs[1])
+        assert errs[0] is not None and "did not join" in str(errs[0])
+        assert elapsed < 30, f"peer waited {elapsed:.1f} s"
+        torch.cuda.synchronize()
+    finally:
+        ranks.close()

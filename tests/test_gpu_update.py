@@ -804,3 +804,32 @@ def test_update_workspace_at_any_alignment(shift):
         outs.append(tab)
     assert torch.equal(outs[0], outs[1])
     assert not torch.equal(outs[0], dev(base))
+
+
+@pytest.mark.parametrize("kind", ["f32", "f64", "f16", "bf16"])
+def test_default_mode_is_exact_where_fast(oracle, kind):
+    """The default update (exact=None, ET_FLAG_EXACT_IF_FAST) is the exact mode for Float32
+    tables — the serial-chain path — and the split mode for the other dtypes, whose exact
+    mode would sum a hot column in one wave: the default's result equals
+    exact=True for f32 and exact=False otherwise, bit for bit."""
+    rng = np.random.default_rng(11)
+    ncols, B, P, dim = 64, 512, 8, 64
+    to = (lambda a: a.astype(np.float32)) if kind == "f32" else (lambda a: a)
+    base = to(_typed(rng, (ncols, dim), "f64" if kind == "f32" else kind))
+    delta = to(_typed(rng, (B, dim), "f64" if kind == "f32" else kind))
+    I = rng.integers(1, ncols + 1, (B, P))
+    I[:, :3] = 5  # a column of 1536+ occurrences: split and exact differ
+    dk = "f32" if kind == "f32" else kind
+    res = {}
+    for mode in (None, True, False):
+        A = et.SimpleEmbedding(dev(base) if dk == "f32" else _dev_typed(base, dk), et.Static(dim))
+        g = et.SparseEmbeddingUpdate(A.lookup_type,
+                                     dev(delta) if dk == "f32" else _dev_typed(delta, dk), dev(I))
+        et.update_(et.Descent(0.1), A, g, exact=mode)
+        res[mode] = _host_bits(A.data)
+    want = res[True] if kind == "f32" else res[False]
+    assert bits_equal(res[None], want)
+    if kind == "f32":
+        ref = base.copy()
+        oracle.sgd(ref, delta, I, 0.1, fused=True)
+        assert bits_equal(res[None], ref)
