@@ -64,6 +64,8 @@ struct KeyGrid {
     uint32_t blk_off[ET_MAX_TABLES_PER_LAUNCH + 1];
     uint32_t in_b;  // bit t: table t's pairs go to the second sort buffer (see et_sort.hip)
     uint32_t vec;   // bit t: contiguous 16-B aligned indices and 16-B aligned pair slots
+    uint32_t snap_mask;  // bit t: copy table t's indices to snap[t] (et_sparse_sgd_snap)
+    int64_t* snap[ET_MAX_TABLES_PER_LAUNCH];  // contiguous pool x batch Int64 copies
 };
 
 // 4 occurrences per thread: two 16-byte index loads, one 16-byte key and one 16-byte
@@ -88,11 +90,18 @@ __global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg,
     const uint32_t nblk = kg.blk_off[t + 1] - kg.blk_off[t];
     int bad = 0;
     uint32_t ol0 = (blockIdx.x - kg.blk_off[t]) * 256u + threadIdx.x;
+    // the snapshot of the indices for indexers[t] (written beside the keys: the index
+    // array is read once, 8 more bytes written per occurrence)
+    int64_t* __restrict__ snap = (kg.snap_mask >> t) & 1u ? kg.snap[t] : nullptr;
     if ((kg.vec >> t) & 1u) {  // workgroup-uniform
         const uint32_t n4 = n_t / 4u;
         const i64x2* ip = reinterpret_cast<const i64x2*>(d.idx);
         for (uint32_t q = ol0; q < n4; q += nblk * 256u) {
             const i64x2 a = ip[2 * q], b = ip[2 * q + 1];
+            if (snap) {  // 16-byte aligned by the host's check
+                reinterpret_cast<i64x2*>(snap)[2 * q] = a;
+                reinterpret_cast<i64x2*>(snap)[2 * q + 1] = b;
+            }
             const uint64_t c[4] = {(uint64_t)(a.x - 1), (uint64_t)(a.y - 1), (uint64_t)(b.x - 1),
                                    (uint64_t)(b.y - 1)};
             u32x4 kv, vv;
@@ -113,7 +122,9 @@ __global__ __launch_bounds__(256) void k_build_keys(UpdatePack pack, KeyGrid kg,
     }
     for (uint32_t ol = ol0; ol < n_t; ol += nblk * 256u) {
         const uint32_t j = ol / pool, i = ol - j * pool;
-        const uint64_t col = (uint64_t)(d.idx[(int64_t)j * d.ld_idx + i] - 1);
+        const int64_t raw = d.idx[(int64_t)j * d.ld_idx + i];
+        if (snap) snap[ol] = raw;
+        const uint64_t col = (uint64_t)(raw - 1);
         const bool ok = col < nr;
         bad += ok ? 0 : 1;
         keys[o0 + ol] = ok ? r0 + (uint32_t)col : sent;
@@ -1309,7 +1320,8 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ tcnt,
                                                       uint32_t* __restrict__ cnt,
                                                       uint2* __restrict__ info,
-                                                      ChainCol* __restrict__ chains) {
+                                                      ChainCol* __restrict__ chains,
+                                                      int kmax) {
     const uint32_t M = counters[kCntM], T = counters[kCntT];
     const int lane = threadIdx.x & 63;
     for (uint32_t m = blockIdx.x * 4 + (threadIdx.x >> 6); m < M; m += gridDim.x * 4) {
@@ -1332,7 +1344,7 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
         for (int k = 0; k < 5; ++k) {
             E[k] = wave_sum_u32(E[k]);
             const uint64_t c = (uint64_t)E[k] * chain_entry_cost2(1u << k);
-            if (c < bc) bc = c, best = k;
+            if (k <= kmax && c < bc) bc = c, best = k;  // kmax 0: every entry one occurrence
         }
         if (lane == 0) {
             cnt[m] = cdiv_u32(E[best], kChainGroup) * kChainGroup + kChainPad;
@@ -1630,7 +1642,7 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
                                                  uint2* __restrict__ info,
                                                  ChainCol* __restrict__ chains,
                                                  uint32_t* __restrict__ ent,
-                                                 uint32_t* __restrict__ counters) {
+                                                 uint32_t* __restrict__ counters, int kmax) {
     const int lane = threadIdx.x & 63;
     const uint32_t M = ec.col0[ec.n];
     const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -1652,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         const uint64_t cc = (uint64_t)v[1 + k] * chain_entry_cost2(1u << k);
-        if (cc < bc) bc = cc, best = k;
+        if (k <= kmax && cc < bc) bc = cc, best = k;
     }
     const bool is_chain = v[0] > chunk;  // wave-uniform
     const uint32_t S = is_chain ? (1u << best) : 0u, E = is_chain ? v[1 + best] : 0u;
@@ -1846,10 +1858,10 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
     const uint32_t quarter = it4 % (uint32_t)kQuadItems, it = it4 / (uint32_t)kQuadItems;
     const ChainCol c = chains[order[it / (uint32_t)ns]];
     if (c.S == 0u) return;
-    // the quad walk for long S = 1 chains only (how >> 2 = the minimum in 64-entry groups):
+    // the quad walk for long S = 1 chains only (how >> 4 = the minimum in 64-entry groups):
     // it spends 4 waves where the 64-feature loop spends one, so short chains, which are
     // throughput- rather than latency-bound, keep the loop; how & 2 turns it off
-    const bool quad = c.S == 1u && (how & 3) == 0 && c.ngr >= ((uint32_t)how >> 2);
+    const bool quad = c.S == 1u && (how & 3) == 0 && c.ngr >= ((uint32_t)how >> 4);
     if (!quad && quarter != 0u) return;
     const int t = table_of_key(pack, ntables, c.key);
     const et_update_desc& d = pack.d[t];
@@ -1901,8 +1913,14 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
             case 1: acc = chain_walk_asm<1>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
             case 2: acc = chain_walk_asm<2>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
             case 4: acc = chain_walk_asm<4>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
-            case 8: acc = chain_walk_asm<8>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
-            default: acc = chain_walk_asm<16>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+            case 8:
+                acc = how & 4 ? chain_walk_ring<8>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f)
+                              : chain_walk_asm<8>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f);
+                break;
+            default:
+                acc = how & 4 ? chain_walk_ring<16>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f)
+                              : chain_walk_asm<16>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f);
+                break;
         }
     }
     if (f < d.dim) {
@@ -1921,6 +1939,15 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
 // its 4 SIMDs.  Top priority: the co-resident chunk-pass / singles / index-phase waves
 // (memory bound) take the leftover issue slots.
 constexpr uint32_t kChainReserveLds = 84 * 1024;  // > 80 KiB: one chain workgroup per CU
+
+// ET_CHAIN_FED=1: chains planned at S = 1 and walked by k_sgd_chains_fed (below).
+inline bool chain_fed() {
+    static const bool v = [] {
+        const char* e = getenv("ET_CHAIN_FED");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
 
 // Helper-fed chains ("HF": the longest early chains, whose runs are long — S >= 8 — and
 // whose columns have at least kHfMinOcc occurrences).  The plain loop spends, per entry of
@@ -2134,6 +2161,176 @@ __global__ __launch_bounds__(256) void k_sgd_chains_x(
         it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
         if (it >= items) break;
         sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it, plain);
+    }
+    __builtin_amdgcn_s_setprio(0);
+}
+
+// ---- Fed chains (round 4, ET_CHAIN_FED): every chain planned at S = 1 — its entry list
+// is the column's occurrence list, one gradient column (bag) per occurrence, in order, padded
+// to whole 64-entry chunks with bag = batch (loads +0) — and walked by a workgroup of four
+// waves: wave 0 sums, waves 1-3 gather.  A gatherer takes every third 64-occurrence chunk,
+// loads its 64 gradient rows as 16 b128 loads (16 lanes per row: lane 16q + i holds
+// features 4i..4i+3 of occurrence 4k + q of group k; the chunk's entries are loaded
+// permuted so DPP row_newbcast:k hands row q its bag) with two chunks in flight, and writes
+// them TRANSPOSED into an LDS ring of kFedSlots occurrence slots (row = feature, slot =
+// occurrence), then publishes the chunk in its FULL word.  The summing wave reads four
+// slots of its feature per ds_read_b128 and adds them in order — exactly the reference's
+// serial sum (src/sparseupdate.jl:110-127), one add per occurrence and no masked slots —
+// and publishes the slots it has consumed (FREE) so gatherers can reuse them.  Per
+// occurrence the summing wave issues one add and a quarter of a read, against S + 5.5 issue
+// slots per entry of r <= S adds (about 1.7 per add on config 4's hottest column) in the
+// one-wave loop, and the gather depth is 3 waves x 2 chunks = 384 occurrences instead of 64.
+constexpr int kFedSlots = 512;              // ring slots (8 chunks of 64 occurrences)
+constexpr int kFedPitch = kFedSlots + 4;    // dwords per feature row: 516 = 4 mod 64, so the
+                                            // 16 lanes of a b128 read hit distinct banks
+constexpr uint32_t kFedLds = 64u * kFedPitch * 4u;  // the ring rows (132 KB; the control
+                                                    // words are a static LDS array)
+enum { kFedFree = 3, kFedItem = 4 };        // control words: FULL[3], FREE, item
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int K>
+__device__ __forceinline__ void fed_issue(f32x4 (&x)[16], uint32_t ev, __amdgpu_buffer_rsrc_t rx,
+                                          uint32_t ld4, uint32_t fbyte) {
+    if constexpr (K < 16) {
+        // row_newbcast writes every lane: mov_dpp with bound_ctrl needs no "old" value
+        const uint32_t bag =
+            (uint32_t)__builtin_amdgcn_mov_dpp((int)ev, 0x150 + K, 0xf, 0xf, true) & 0xffffffu;
+        x[K] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rx, (int)(__umul24(bag, ld4) + fbyte), 0, 0));
+        fed_issue<K + 1>(x, ev, rx, ld4, fbyte);
+    }
+}
+
+// The control words live in a static LDS array and are read and written with workgroup-
+// scope relaxed atomics, so they compile to ds_read / ds_write (a volatile generic pointer
+// becomes flat_load / flat_store, whose vmcnt waits would drain the gatherers' loads).
+__device__ __forceinline__ uint32_t fed_get(uint32_t* ctl, int i) {
+    return __hip_atomic_load(ctl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void fed_set(uint32_t* ctl, int i, uint32_t v) {
+    __hip_atomic_store(ctl + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Gatherer: chunk ch's 64 rows from x into ring position ch % 8, then FULL[p] = ch / 3 + 1.
+__device__ __forceinline__ void fed_put(const f32x4 (&x)[16], float* lds, uint32_t* ctl,
+                                        uint32_t ch, int p, int lane) {
+    if (ch >= (uint32_t)(kFedSlots / 64)) {  // the ring position held chunk ch - 8
+        const uint32_t need = (ch + 1u - (uint32_t)(kFedSlots / 64)) * 64u;
+        while (fed_get(ctl, kFedFree) < need) __builtin_amdgcn_s_sleep(1);
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const int q = lane >> 4, i = lane & 15;
+    float* base = lds + (4 * i) * kFedPitch + (int)(ch % (uint32_t)(kFedSlots / 64)) * 64 + q;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        base[4 * k] = x[k].x;
+        base[kFedPitch + 4 * k] = x[k].y;
+        base[2 * kFedPitch + 4 * k] = x[k].z;
+        base[3 * kFedPitch + 4 * k] = x[k].w;
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) fed_set(ctl, p, ch / 3u + 1u);  // a wave's LDS operations complete in order
+}
+
+template <int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_chains_fed(
+    UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
+    const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ uint32_t ctl[8];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t items = counters[kCntM] * (uint32_t)ns;
+    __builtin_amdgcn_s_setprio(3);
+    for (;;) {
+        if (threadIdx.x == 0) {
+            fed_set(ctl, 0, 0u);
+            fed_set(ctl, 1, 0u);
+            fed_set(ctl, 2, 0u);
+            fed_set(ctl, kFedFree, 0u);
+            fed_set(ctl, kFedItem, atomicAdd(&counters[kCntNext], 1u));
+        }
+        __syncthreads();
+        const uint32_t it = (uint32_t)__builtin_amdgcn_readfirstlane((int)fed_get(ctl, kFedItem));
+        if (it >= items) break;  // workgroup-uniform
+        const ChainCol c = chains[order[it / (uint32_t)ns]];
+        const int slice = (int)(it % (uint32_t)ns);
+        const int t = table_of_key(pack, ntables, c.key);
+        const et_update_desc& d = pack.d[t];
+        const uint32_t nch = c.ngr;
+        if (c.S != 0u && slice * 64 < d.dim && nch > 0u) {  // workgroup-uniform
+            if (wave == 0) {  // the serial sum
+                float acc = 0.0f;
+                const float* row = lds + lane * kFedPitch;
+                for (uint32_t ch = 0; ch < nch; ++ch) {
+                    const uint32_t need = ch / 3u + 1u;
+                    while (fed_get(ctl, (int)(ch % 3u)) < need) __builtin_amdgcn_s_sleep(0);
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    const f32x4* src = reinterpret_cast<const f32x4*>(
+                        row + (int)(ch % (uint32_t)(kFedSlots / 64)) * 64);
+                    f32x4 v[16];
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) v[m] = src[m];
+#pragma unroll
+                    for (int m = 0; m < 16; ++m) {
+                        acc = acc + v[m].x;
+                        acc = acc + v[m].y;
+                        acc = acc + v[m].z;
+                        acc = acc + v[m].w;
+                    }
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    if (lane == 0) fed_set(ctl, kFedFree, (ch + 1u) * 64u);
+                }
+                const int f = slice * 64 + lane;
+                if (f < d.dim) {
+                    float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
+                                              c.key - pack.row_off[t]) + f;
+                    store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+                }
+            } else {  // gatherer p: chunks p, p + 3, ...
+                const int p = wave - 1;
+                const uint32_t ld = (uint32_t)d.ld_delta;
+                const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<void*>(d.delta), 0, (int)((uint32_t)d.batch * ld * 4u), 0x00020000);
+                const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint32_t*>(ent + c.e0), 0, (int)(nch * 256u), 0x00020000);
+                // lane 16q + i loads entry 4i + q of a chunk (row_newbcast:k -> entry 4k + q)
+                const uint32_t poff = 4u * (4u * (uint32_t)(lane & 15) + (uint32_t)(lane >> 4));
+                const uint32_t fbyte = 4u * (uint32_t)(slice * 64 + 4 * (lane & 15));
+                const uint32_t ld4 = 4u * ld;
+                // this gatherer's chunks: i = 0, 1, .. is chunk p + 3i.  Issue order per
+                // step i: entries of chunk i+3, put chunk i (waits for its rows), rows of
+                // chunk i+2 into the freed buffer — so the entries a row load needs were
+                // issued before the previous chunk's rows and never drain them (loads
+                // complete in order); two row buffers and two entry registers alternate
+                // by step parity (no copies of registers with loads in flight)
+                const uint32_t nm = (uint32_t)p < nch ? (nch - (uint32_t)p + 2u) / 3u : 0u;
+                // unconditional: a chunk past the list is past the entries' range (loads 0)
+                auto entries = [&](uint32_t i) {
+                    return __builtin_amdgcn_raw_buffer_load_b32(
+                        re, (int)(((uint32_t)p + 3u * i) * 256u + poff), 0, 0);
+                };
+                f32x4 xa[16], xb[16];
+                const uint32_t e0v = entries(0u), e1v = entries(1u);
+                fed_issue<0>(xa, e0v, rx, ld4, fbyte);
+                fed_issue<0>(xb, e1v, rx, ld4, fbyte);
+                uint32_t ra = entries(2u), rb = 0u;
+                // the row loads are unconditional (past the list the entries load 0: row 0,
+                // never put), so every pending load is consumed on every path and the
+                // compiler's wait counts stay partial across the loop's back edge
+                for (uint32_t i = 0; i < nm; i += 2u) {
+                    fed_put(xa, lds, ctl, (uint32_t)p + 3u * i, p, lane);
+                    rb = entries(i + 3u);
+                    fed_issue<0>(xa, ra, rx, ld4, fbyte);
+                    if (i + 1u >= nm) break;
+                    fed_put(xb, lds, ctl, (uint32_t)p + 3u * (i + 1u), p, lane);
+                    ra = entries(i + 4u);
+                    fed_issue<0>(xb, rb, rx, ld4, fbyte);
+                }
+            }
+        }
+        __syncthreads();  // the ring and the control words are free for the next item
     }
     __builtin_amdgcn_s_setprio(0);
 }
@@ -2375,20 +2572,27 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
 inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s,
                              uint32_t hot_mask = 0, const HotList* hl = nullptr,
-                             bool chain = false, uint32_t ec_mask = 0) {
+                             bool chain = false, uint32_t ec_mask = 0,
+                             int64_t* const* snaps = nullptr) {
     const int64_t blocks = cdiv64(n, 256);
     const unsigned kb_grid = (unsigned)(blocks < 65536 ? blocks : 65536);
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
     KeyGrid kg;
     kg.blk_off[0] = 0;
     kg.vec = 0;
+    kg.snap_mask = 0;
+    for (int t = 0; t < ntables; ++t) {
+        kg.snap[t] = snaps ? snaps[t] : nullptr;
+        if (kg.snap[t]) kg.snap_mask |= 1u << t;
+    }
     const bool bufs16 = (((uintptr_t)w.ka | (uintptr_t)w.va | (uintptr_t)w.kb | (uintptr_t)w.vb) &
                          15u) == 0;
     for (int t = 0; t < ntables; ++t) {
         const int64_t nt = pack.occ_off[t + 1] - pack.occ_off[t];
         const et_update_desc& d = pack.d[t];
         const bool vec = bufs16 && (d.ld_idx == d.pool || d.batch == 1) &&
-                         ((uintptr_t)d.idx & 15u) == 0 && (pack.occ_off[t] & 3u) == 0;
+                         ((uintptr_t)d.idx & 15u) == 0 && (pack.occ_off[t] & 3u) == 0 &&
+                         ((uintptr_t)kg.snap[t] & 15u) == 0;
         if (vec) kg.vec |= 1u << t;
         int64_t nb = cdiv64(nt, vec ? 1024 : 256);
         nb = nb < 2048 ? nb : 2048;  // grid-stride beyond 2048 workgroups per table
@@ -2447,7 +2651,7 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
                            w.chain_tile_col, w.chain_tcnt);
         hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
                            w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
-                           w.chain_info, w.chains);
+                           w.chain_info, w.chains, chain_fed() ? 0 : 4);
         hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
                            w.chain_info, w.chain_e0, w.chain_order);
         hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
@@ -2544,8 +2748,10 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         const char* e = getenv("ET_CHAIN_ASM");
         const char* q = getenv("ET_CHAIN_QUAD");
         const char* m = getenv("ET_QUAD_MIN");  // experiments: quad-walk threshold
+        const char* r = getenv("ET_CHAIN_RING");  // S >= 8: the 64-deep ring loop
         const int qmin = m ? atoi(m) : kQuadMinGroups;
-        return (e && atoi(e) == 0 ? 1 : 0) | (q && atoi(q) == 0 ? 2 : 0) | (qmin << 2);
+        return (e && atoi(e) == 0 ? 1 : 0) | (q && atoi(q) == 0 ? 2 : 0) |
+               (r && atoi(r) != 0 ? 4 : 0) | (qmin << 4);
     }();
     // experiments: ET_CHAIN_LDS = KiB reserved per chain workgroup (160: a whole CU)
     static const uint32_t lds = [] {
@@ -2569,6 +2775,16 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
     else
         ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
     ET_HIP_CHECK(hipMemsetAsync(counters + kCntHfNext, 0, 4, s));
+    if (chain_fed()) {  // every chain planned at S = 1: the fed walk
+        static const hipError_t attr_f = hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&k_sgd_chains_fed<MODE, NT>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFedLds);
+        ET_HIP_CHECK(attr_f);
+        hipLaunchKernelGGL((k_sgd_chains_fed<MODE, NT>), dim3(nb), dim3(256), kFedLds, s, pack,
+                           ntables, counters, chains, order, ent, ns, eta32, eta64);
+        ET_LAUNCH_CHECK("k_sgd_chains_fed");
+        return ET_OK;
+    }
     if (excl && nhf == 0) {
         hipLaunchKernelGGL((k_sgd_chains_x<MODE, NT>), dim3(nb), dim3(256), lds, s, pack,
                            ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64,
@@ -2942,7 +3158,7 @@ inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chu
     hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_stats);
     hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
                        w.ec_stats, w.ec_boff, w.ec_cnt, w.ec_nocc, w.ec_info, w.ec_chains,
-                       w.ec_ent, w.ec_counters);
+                       w.ec_ent, w.ec_counters, chain_fed() ? 0 : 4);
     hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.ec_info, w.ec_nocc, ns,
                        w.ec_order, w.ec_counters);
     hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_boff,
@@ -2975,9 +3191,30 @@ extern "C" int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntable
     return ET_OK;
 }
 
+static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
+                      uint32_t flags, int64_t* const* snaps, void* workspace, int64_t ws_bytes,
+                      void* stream);
+
 extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
                              uint32_t flags, void* workspace, int64_t ws_bytes, void* stream) {
     et::clear_err();
+    return sparse_sgd(dtype, descs, ntables, eta, flags, nullptr, workspace, ws_bytes, stream);
+}
+
+extern "C" int et_sparse_sgd_snap(int dtype, const et_update_desc* descs, int32_t ntables,
+                                  double eta, uint32_t flags, int64_t* const* snaps,
+                                  void* workspace, int64_t ws_bytes, void* stream) {
+    et::clear_err();
+    if (!snaps) return et::fail(ET_ERR_ARG, "snaps is NULL");
+    if (ntables > ET_MAX_TABLES_PER_LAUNCH)
+        return et::fail(ET_ERR_ARG, "et_sparse_sgd_snap: at most %d tables per call",
+                        ET_MAX_TABLES_PER_LAUNCH);
+    return sparse_sgd(dtype, descs, ntables, eta, flags, snaps, workspace, ws_bytes, stream);
+}
+
+static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
+                      uint32_t flags, int64_t* const* snaps, void* workspace, int64_t ws_bytes,
+                      void* stream) {
     if (dtype != ET_F32 && dtype != ET_F64 && dtype != ET_F16 && dtype != ET_BF16)
         return et::fail(ET_ERR_UNSUPPORTED, "sparse SGD: dtype %d", dtype);
     const bool index_only = (flags & ET_FLAG_SGD_INDEX_ONLY) != 0;
@@ -3089,7 +3326,7 @@ extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t nta
         gr = et::grouped_pairs(pack, ntables, w);  // phase 1 ran earlier in stream order
     } else {
         rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s, hot_mask, &hl, chain,
-                                   use_ec ? ec.mask : 0u);
+                                   use_ec ? ec.mask : 0u, snaps);
         if (rc != ET_OK || index_only) return rc;
     }
     et::ChainRun cr;

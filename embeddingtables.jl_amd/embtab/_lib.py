@@ -52,6 +52,7 @@ EXPORTS = (
     "et_maplookup_prealloc_to",
     "et_sgd_workspace_size",
     "et_sparse_sgd",
+    "et_sparse_sgd_snap",
     "et_index_workspace_size",
     "et_index_build",
     "et_update_indexed",
@@ -153,6 +154,7 @@ def load() -> ctypes.CDLL:
         "et_maplookup_prealloc_to": ([c_int, c_int, vp, i32, i64, vp, i64, u32, vp], c_int),
         "et_sgd_workspace_size": ([vp, i32, vp], c_int),
         "et_sparse_sgd": ([c_int, vp, i32, dbl, u32, vp, i64, vp], c_int),
+        "et_sparse_sgd_snap": ([c_int, vp, i32, dbl, u32, vp, vp, i64, vp], c_int),
         "et_index_workspace_size": ([i64, vp], c_int),
         "et_index_build": ([vp, i32, i64, i64, i64, vp, vp, vp, vp, vp, i64, vp], c_int),
         "et_update_indexed": ([c_int, vp, i64, i64, i64, i32, vp, i64, vp, vp, i64, i64, vp, dbl, u32,

@@ -214,6 +214,18 @@ int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntables, int64_t*
 int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
                   uint32_t flags, void* workspace, int64_t ws_bytes, void* stream);
 
+/* et_sparse_sgd that also copies every table's indices as its index phase reads them (ABI
+ * v8): snaps is a HOST array of ntables (<= ET_MAX_TABLES_PER_LAUNCH) device pointers;
+ * snaps[t] != NULL receives table t's pool x batch Int64 indices, contiguous (bag-major),
+ * stream-ordered inside the index phase (not written by an APPLY_ONLY call).  The copy the
+ * multi-table update!(opt, tables, grads, indexers) keeps for filling indexers[i]
+ * (src/sparseupdate.jl:210-213) when the caller may refill the index buffers before reading
+ * them: 8 bytes written per occurrence beside the keys instead of a separate read-and-write
+ * pass.  16-byte aligned snapshots keep the vectorized key pass. */
+int et_sparse_sgd_snap(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
+                       uint32_t flags, int64_t* const* snaps, void* workspace, int64_t ws_bytes,
+                       void* stream);
+
 /* Update from a prebuilt Indexer (et_index_build layout) over its cumulative entries
  * [ubegin, uend) — the reference's lower-level
  * update!(table, ::SparseEmbeddingUpdate, indexer::AbstractIndexer, alpha, Val(NT)),
