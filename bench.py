@@ -211,6 +211,41 @@ def _timed(fn, steps, warmup, stream):
     return sum(a.elapsed_time(b) for a, b in ev) / steps
 
 
+def table_classes(et, tables, idx, tids, batch, stream, mixed_ms, steps=10, warmup=3):
+    """The headline launch split by table class: every class's tables
+    alone in one Preallocation launch of their own — heavy (> 256 MiB, rows from HBM), mid
+    (4 MiB .. 256 MiB, Infinity-Cache resident), light (<= 4 MiB, one XCD's L2) — with its
+    time, its §8d algorithmic rate and (heavy) its HBM-compulsory rate, so the gap between
+    the mixed launch and the HBM roofline is traceable to a class."""
+    import torch
+
+    out = {}
+    classes = (("heavy", lambda b: b > INFINITY_CACHE), ("mid", lambda b: (4 << 20) < b <= INFINITY_CACHE),
+               ("light", lambda b: b <= (4 << 20)))
+    total = 0.0
+    for name, pick in classes:
+        sel = [k for k, t in enumerate(tids) if pick(CRITEO_KAGGLE_ROWS[t] * DIM * 4)]
+        if not sel:
+            continue
+        tabs = [tables[k] for k in sel]
+        ids = [idx[k] for k in sel]
+        dst = torch.empty((batch, DIM * len(sel)), dtype=torch.float32, device=tables[0].data.device)
+        strat = et.PreallocationStrategy(0)
+        ms = _timed(lambda: et.maplookup_(strat, dst, tabs, ids), steps, warmup, stream)
+        rows = [CRITEO_KAGGLE_ROWS[tids[k]] for k in sel]
+        alg = algorithmic_bytes(batch, POOL, [DIM] * len(sel))
+        hbm = hbm_compulsory_bytes(batch, POOL, [DIM] * len(sel), rows)
+        out[name] = {"tables": len(sel), "ms_alone": ms,
+                     "algorithmic_GBs": alg / (ms * 1e-3) / 1e9,
+                     "hbm_compulsory_GBs": hbm / (ms * 1e-3) / 1e9,
+                     "hbm_compulsory_frac": hbm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        total += ms
+        del dst
+    out["sum_alone_ms"] = total
+    out["mixed_ms"] = mixed_ms
+    return out
+
+
 def bench_config2(et, L, device, steps, warmup, nsets=16):
     """BASELINE configs[1]: one 128 x 1e7 fp32 table, vector-index (non-reducing) gather,
     B = 65536.  Bytes per lookup: 512 read + 512 written + 8 index.
@@ -708,6 +743,9 @@ def main():
             "kernel_ms_median": kernel_ms_median,
         },
     }
+    if not sharded and world == 1 and not args.no_extra:
+        result["roofline"]["classes"] = table_classes(et, tables, idx, mine, B, stream,
+                                                      kernel_ms)
     if sharded:
         result["lookup_only_ms"] = kernel_ms
         result["slab_cols"] = plan.slab_ld

@@ -287,6 +287,24 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
 // only 512-byte rows take this loop.
 typedef const __attribute__((address_space(4))) int64_t* cidx_ptr;
 
+// Bytes per lane of the scalar-addressed loop: 16 for 512-byte rows, 8 for 256-byte rows
+// (D = 128 fp16 / bf16, 64 fp32): two bags per wave either way — half a wave per row —
+// so both bags stay wave-uniform and their indices scalar.  (Round 2 tried 256-byte rows
+// as FOUR bags per wave with 16-byte lanes: the four scalar index streams stalled each
+// batch, and it was slower than load_add.)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <int BPL> struct SgVec { typedef u32x4 type; };
+template <> struct SgVec<8> { typedef u32x2 type; };
+template <typename T> constexpr int sg_bpl(int D) { return D * (int)sizeof(T) / 32; }
+
+template <bool NT, typename V>
+__device__ __forceinline__ void store_v(V* p, V v) {
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
 __device__ __forceinline__ cidx_ptr as_scalar_idx(const int64_t* p) {
     return (cidx_ptr)(uintptr_t)p;
 }
@@ -309,12 +327,14 @@ __device__ __forceinline__ uint64_t row_off_s(int64_t v, uint32_t ldb, uint32_t 
 // One batch of UU rows of both bags.  Returns false — before issuing any row load —
 // if an index of the batch is out of range; the caller then redoes the bag pair with
 // bag_pair_checked.
-template <typename T, typename A, int UU, bool NTL>
+template <typename T, typename A, int UU, bool NTL, int BPL = 16>
 __device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t nrows,
                                            cidx_ptr ia, cidx_ptr ib, uint64_t hmask,
                                            uint64_t lane_off, bool first_batch,
-                                           A (&acc)[16 / sizeof(T)]) {
-    constexpr int N = 16 / (int)sizeof(T);
+                                           A (&acc)[BPL / sizeof(T)]) {
+    constexpr int N = BPL / (int)sizeof(T);
+    typedef typename SgVec<BPL>::type V;
+    typedef const __attribute__((address_space(1))) V gvec;
     // lane address = table + row_off(A) + (hi ? row_off(B) - row_off(A) : 0) + 16*sub:
     // the difference is masked per lane (hmask = ~0 in lanes 32-63), so a row pair costs
     // two v_and and two 64-bit adds — no 64-bit selects between scalar operands
@@ -326,11 +346,11 @@ __device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t 
         dd[u] = row_off_s(ib[u], ldb, nrows, bad) - oa[u];
     }
     if (bad) return false;
-    u32x4 buf[UU];
+    V buf[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         const uint64_t a = ((dd[u] & hmask) + lane_off) + (tb + oa[u]);
-        const gvec16* src = reinterpret_cast<const gvec16*>(a);
+        const gvec* src = reinterpret_cast<const gvec*>(a);
         if constexpr (NTL)
             buf[u] = __builtin_nontemporal_load(src);
         else
@@ -339,7 +359,7 @@ __device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t 
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
         T x[N];
-        unpack16<T, N>(buf[u], x);
+        __builtin_memcpy(x, &buf[u], BPL);
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             if (u == 0)
@@ -353,39 +373,42 @@ __device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t 
 
 // The bag pair again, one row at a time with per-lane range checks: an out-of-range
 // index contributes a zero row and is counted (the reference leaves it undefined).
-template <typename T, typename A>
+template <typename T, typename A, int BPL = 16>
 __device__ __forceinline__ void bag_pair_checked(uintptr_t tb, uint32_t ldb, uint32_t nrows,
                                                  const int64_t* ia, const int64_t* ib, bool hi,
                                                  int sub, int pool, A* acc, int* bad) {
-    constexpr int N = 16 / (int)sizeof(T);
+    constexpr int N = BPL / (int)sizeof(T);
+    typedef typename SgVec<BPL>::type V;
     const int64_t* ip = hi ? ib : ia;
 #pragma unroll 1
     for (int i = 0; i < pool; ++i) {
         const uint64_t r = (uint64_t)(ip[i] - 1);
         const bool ok = r < (uint64_t)nrows;
         *bad += ok ? 0 : 1;
-        const u32x4 v = *(reinterpret_cast<const u32x4*>(
-                              tb + (uint64_t)(ok ? (uint32_t)r : 0u) * ldb) + sub);
+        const V v = *(reinterpret_cast<const V*>(
+                          tb + (uint64_t)(ok ? (uint32_t)r : 0u) * ldb) + sub);
         T x[N];
-        unpack16<T, N>(ok ? v : u32x4{0u, 0u, 0u, 0u}, x);
+        const V z = ok ? v : V(0u);
+        __builtin_memcpy(x, &z, BPL);
         for (int k = 0; k < N; ++k) acc[k] = i == 0 ? A(x[k]) : A(acc[k] + A(x[k]));
     }
 }
 
 // `rounds` rounds of 8 bags per workgroup (bag mapping identical to run_bags: wave w
 // of round r holds bags chunk*8*rounds + r*8 + 2w + {0, 1}).
-template <typename T, typename A, int U, bool NT, bool NTL>
+template <typename T, typename A, int U, bool NT, bool NTL, int BPL = 16>
 __device__ __forceinline__ void run_bags_s(const et_lookup_desc& d, int64_t batch,
                                            T* __restrict__ dst, int64_t ld_dst, int64_t chunk,
                                            int rounds) {
-    constexpr int N = 16 / (int)sizeof(T);
+    constexpr int N = BPL / (int)sizeof(T);
+    typedef typename SgVec<BPL>::type V;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool hi = lane >= 32;
     const int sub = lane & 31;
     uint32_t hm = hi ? ~0u : 0u;
     asm volatile("" : "+v"(hm));  // opaque: keep `dd & hmask` two v_and, not selects
-    const uint64_t hmask = ((uint64_t)hm << 32) | hm, lane_off = (uint64_t)sub * 16u;
+    const uint64_t hmask = ((uint64_t)hm << 32) | hm, lane_off = (uint64_t)sub * (uint64_t)BPL;
     const uintptr_t tb = reinterpret_cast<uintptr_t>(d.table);
     const uint32_t ldb = (uint32_t)(d.ld_table * (int64_t)sizeof(T)), nr = (uint32_t)d.nrows;
     const int pool = d.pool;
@@ -401,7 +424,7 @@ __device__ __forceinline__ void run_bags_s(const et_lookup_desc& d, int64_t batc
         bool ok = true;
         int i0 = 0;
 #define ET_LOAD_ADD_S(UU) \
-    load_add_s<T, A, UU, NTL>(tb, ldb, nr, ia + i0, ib + i0, hmask, lane_off, i0 == 0, acc)
+    load_add_s<T, A, UU, NTL, BPL>(tb, ldb, nr, ia + i0, ib + i0, hmask, lane_off, i0 == 0, acc)
         for (; ok && i0 + U <= pool; i0 += U) ok = ET_LOAD_ADD_S(U);
         if constexpr (U > 4) {
             if (ok && pool - i0 >= 4) {
@@ -419,7 +442,7 @@ __device__ __forceinline__ void run_bags_s(const et_lookup_desc& d, int64_t batc
 #undef ET_LOAD_ADD_S
         int bad = 0;
         if (!ok)
-            bag_pair_checked<T, A>(tb, ldb, nr, d.idx + bag * d.ld_idx,
+            bag_pair_checked<T, A, BPL>(tb, ldb, nr, d.idx + bag * d.ld_idx,
                                    d.idx + (has_b ? bag + 1 : bag) * d.ld_idx, hi, sub, pool, acc,
                                    &bad);
         if (hi && !has_b) bad = 0;  // the upper half re-ran bag A: counted by the lower
@@ -428,9 +451,10 @@ __device__ __forceinline__ void run_bags_s(const et_lookup_desc& d, int64_t batc
             T y[N];
 #pragma unroll
             for (int k = 0; k < N; ++k) y[k] = T(acc[k]);
-            u32x4* o = reinterpret_cast<u32x4*>(dst + (bag + (hi ? 1 : 0)) * ld_dst +
-                                                d.dst_row_off) + sub;
-            store16<NT>(o, pack16<T, N>(y));
+            V* o = reinterpret_cast<V*>(dst + (bag + (hi ? 1 : 0)) * ld_dst + d.dst_row_off) + sub;
+            V yv;
+            __builtin_memcpy(&yv, y, BPL);
+            store_v<NT>(o, yv);
         }
     }
 }
@@ -446,7 +470,7 @@ __global__ __launch_bounds__(256) void k_pooled_vec(LookupPack pack, int ntables
     const int t = (int)(item % ntables);
     const int64_t chunk = item / ntables;
     if constexpr (SG)
-        run_bags_s<T, A, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+        run_bags_s<T, A, U, NT, false, sg_bpl<T>(D)>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
     else
         run_bags<T, A, D, U, NT, false, false, PG, MK>(pack.d[t], batch, dst, ld_dst, chunk,
                                                        rounds);
@@ -487,9 +511,11 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
     if ((sm.prio_mask >> t) & 1u) __builtin_amdgcn_s_setprio(2);
     if constexpr (SG) {
         if ((sm.ntload_mask >> t) & 1u)
-            run_bags_s<T, A, U, NT, true>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+            run_bags_s<T, A, U, NT, true, sg_bpl<T>(D)>(pack.d[t], batch, dst, ld_dst, chunk,
+                                                         rounds);
         else
-            run_bags_s<T, A, U, NT, false>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
+            run_bags_s<T, A, U, NT, false, sg_bpl<T>(D)>(pack.d[t], batch, dst, ld_dst, chunk,
+                                                          rounds);
     } else {
         if ((sm.ntload_mask >> t) & 1u)
             run_bags<T, A, D, U, NT, true, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
@@ -698,6 +724,7 @@ struct LookupTuning {
     int rows_in_flight = 0;        // ET_U=4|8|16: rows per group in flight (fp32 D=128)
     int w8 = 0;                    // ET_W8=1: the striped kernel held to 8 waves per SIMD
     int sgpr = 1;                  // ET_SGPR=0: 512-byte rows use the per-lane loop too
+    int sg256 = 0;                 // ET_SG256=1: 256-byte rows take the scalar loop too
     int heavy_prio = 0;            // ET_HEAVY_PRIO=1: heavy tables' waves at priority 2
 };
 
@@ -713,6 +740,7 @@ inline const LookupTuning& tuning() {
         if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
         if (const char* e = getenv("ET_W8")) v.w8 = atoi(e);
         if (const char* e = getenv("ET_SGPR")) v.sgpr = atoi(e);
+        if (const char* e = getenv("ET_SG256")) v.sg256 = atoi(e);
         if (const char* e = getenv("ET_HEAVY_PRIO")) v.heavy_prio = atoi(e);
         return v;
     }();
@@ -784,13 +812,15 @@ template <typename T, typename A, int D, int U, bool NT, bool PG, bool MK>
 int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                         hipStream_t s) {
     using G = VecGeom<T, D>;
-    const int64_t per_round = 4 * G::GPW;
+    // the scalar-addressed loop: 512-byte rows, and 256-byte rows with 8-byte lanes (ET_SG256)
+    constexpr bool kSG = !PG && !MK && (D * (int)sizeof(T) == 512 || D * (int)sizeof(T) == 256);
+    bool sg = kSG && tuning().sgpr &&
+              (D * (int)sizeof(T) == 512 || tuning().sg256);  // row strides must fit 32 bits
+    for (int t = 0; t < n && sg; ++t) sg = pack.d[t].ld_table * (int64_t)sizeof(T) < (1ll << 32);
+    const int64_t per_round = sg ? 8 : 4 * G::GPW;  // the scalar loop: two bags per wave
     const int rounds = rounds_for(batch, per_round, n);
     const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
     if (nchunks <= 0) return ET_OK;
-    constexpr bool kSG = !PG && !MK && D * (int)sizeof(T) == 512;
-    bool sg = kSG && tuning().sgpr;  // row strides in bytes must fit 32 bits
-    for (int t = 0; t < n && sg; ++t) sg = pack.d[t].ld_table * (int64_t)sizeof(T) < (1ll << 32);
     if (!PG && !MK && n > 1 && tuning().striped) {
         StripeMap sm;
         build_stripe_map(pack, n, (int)sizeof(T), sm);

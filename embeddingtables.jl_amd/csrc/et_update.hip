@@ -1940,14 +1940,16 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
 // (memory bound) take the leftover issue slots.
 constexpr uint32_t kChainReserveLds = 84 * 1024;  // > 80 KiB: one chain workgroup per CU
 
-// ET_CHAIN_FED=1: chains planned at S = 1 and walked by k_sgd_chains_fed (below).
-inline bool chain_fed() {
-    static const bool v = [] {
+// ET_CHAIN_FED: chains planned at S = 1 and walked by k_sgd_chains_fed (below) — 1: the
+// early chains, 2: the early and the regular chains.
+inline int chain_fed_level() {
+    static const int v = [] {
         const char* e = getenv("ET_CHAIN_FED");
-        return e ? atoi(e) != 0 : false;
+        return e ? atoi(e) : 0;
     }();
     return v;
 }
+inline bool chain_fed(bool early) { return chain_fed_level() >= (early ? 1 : 2); }
 
 // Helper-fed chains ("HF": the longest early chains, whose runs are long — S >= 8 — and
 // whose columns have at least kHfMinOcc occurrences).  The plain loop spends, per entry of
@@ -2167,39 +2169,27 @@ __global__ __launch_bounds__(256) void k_sgd_chains_x(
 
 // ---- Fed chains (round 4, ET_CHAIN_FED): every chain planned at S = 1 — its entry list
 // is the column's occurrence list, one gradient column (bag) per occurrence, in order, padded
-// to whole 64-entry chunks with bag = batch (loads +0) — and walked by a workgroup of four
-// waves: wave 0 sums, waves 1-3 gather.  A gatherer takes every third 64-occurrence chunk,
-// loads its 64 gradient rows as 16 b128 loads (16 lanes per row: lane 16q + i holds
-// features 4i..4i+3 of occurrence 4k + q of group k; the chunk's entries are loaded
-// permuted so DPP row_newbcast:k hands row q its bag) with two chunks in flight, and writes
-// them TRANSPOSED into an LDS ring of kFedSlots occurrence slots (row = feature, slot =
-// occurrence), then publishes the chunk in its FULL word.  The summing wave reads four
-// slots of its feature per ds_read_b128 and adds them in order — exactly the reference's
-// serial sum (src/sparseupdate.jl:110-127), one add per occurrence and no masked slots —
-// and publishes the slots it has consumed (FREE) so gatherers can reuse them.  Per
-// occurrence the summing wave issues one add and a quarter of a read, against S + 5.5 issue
-// slots per entry of r <= S adds (about 1.7 per add on config 4's hottest column) in the
-// one-wave loop, and the gather depth is 3 waves x 2 chunks = 384 occurrences instead of 64.
+// to whole 64-entry chunks with bag = batch (loads +0) — and walked by a workgroup of eight
+// waves: wave 0 sums, waves 1-7 gather.  Gatherer p takes chunks p, p + 7, ...: per
+// occurrence one dword load of the 64-feature row (lane = feature; the bag comes from the
+// chunk's entry vector by v_readlane, the row offset as the scalar offset), issued in halves
+// of 32 occurrences so ~64 loads stay in flight per gatherer (7 x 64 occurrences in all);
+// every 4 occurrences of a feature go to LDS as one ds_write_b128 into that feature's row of
+// an LDS ring of kFedSlots occurrence slots (row = feature, slot = occurrence; pitch 516
+// dwords = 4 mod 64 banks, so both the writes and the summing wave's b128 reads are free of
+// bank conflicts — the first version's per-occurrence b32 writes of 16-byte load slices
+// were 8-way conflicted and bounded the walk at ~16 LDS cycles per occurrence).  A gatherer
+// publishes a chunk in its FULL word; the summing wave reads four slots of its feature per
+// ds_read_b128 and adds them in order — exactly the reference's serial sum
+// (src/sparseupdate.jl:110-127), one add per occurrence and no masked slots — and publishes
+// the slots it has consumed (FREE) so gatherers can reuse them.
 constexpr int kFedSlots = 512;              // ring slots (8 chunks of 64 occurrences)
-constexpr int kFedPitch = kFedSlots + 4;    // dwords per feature row: 516 = 4 mod 64, so the
-                                            // 16 lanes of a b128 read hit distinct banks
+constexpr int kFedPitch = kFedSlots + 4;    // dwords per feature row: 516 = 4 mod 64
+constexpr int kFedGather = 7;               // gatherer waves per workgroup
 constexpr uint32_t kFedLds = 64u * kFedPitch * 4u;  // the ring rows (132 KB; the control
                                                     // words are a static LDS array)
-enum { kFedFree = 3, kFedItem = 4 };        // control words: FULL[3], FREE, item
+enum { kFedFree = kFedGather, kFedItem = kFedGather + 1, kFedCtl = kFedGather + 2 };
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <int K>
-__device__ __forceinline__ void fed_issue(f32x4 (&x)[16], uint32_t ev, __amdgpu_buffer_rsrc_t rx,
-                                          uint32_t ld4, uint32_t fbyte) {
-    if constexpr (K < 16) {
-        // row_newbcast writes every lane: mov_dpp with bound_ctrl needs no "old" value
-        const uint32_t bag =
-            (uint32_t)__builtin_amdgcn_mov_dpp((int)ev, 0x150 + K, 0xf, 0xf, true) & 0xffffffu;
-        x[K] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rx, (int)(__umul24(bag, ld4) + fbyte), 0, 0));
-        fed_issue<K + 1>(x, ev, rx, ld4, fbyte);
-    }
-}
 
 // The control words live in a static LDS array and are read and written with workgroup-
 // scope relaxed atomics, so they compile to ds_read / ds_write (a volatile generic pointer
@@ -2211,44 +2201,20 @@ __device__ __forceinline__ void fed_set(uint32_t* ctl, int i, uint32_t v) {
     __hip_atomic_store(ctl + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Gatherer: chunk ch's 64 rows from x into ring position ch % 8, then FULL[p] = ch / 3 + 1.
-__device__ __forceinline__ void fed_put(const f32x4 (&x)[16], float* lds, uint32_t* ctl,
-                                        uint32_t ch, int p, int lane) {
-    if (ch >= (uint32_t)(kFedSlots / 64)) {  // the ring position held chunk ch - 8
-        const uint32_t need = (ch + 1u - (uint32_t)(kFedSlots / 64)) * 64u;
-        while (fed_get(ctl, kFedFree) < need) __builtin_amdgcn_s_sleep(1);
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const int q = lane >> 4, i = lane & 15;
-    float* base = lds + (4 * i) * kFedPitch + (int)(ch % (uint32_t)(kFedSlots / 64)) * 64 + q;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        base[4 * k] = x[k].x;
-        base[kFedPitch + 4 * k] = x[k].y;
-        base[2 * kFedPitch + 4 * k] = x[k].z;
-        base[3 * kFedPitch + 4 * k] = x[k].w;
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) fed_set(ctl, p, ch / 3u + 1u);  // a wave's LDS operations complete in order
-}
-
 template <int MODE, bool NT>
-__global__ __launch_bounds__(256) void k_sgd_chains_fed(
+__global__ __launch_bounds__(64 * (kFedGather + 1)) void k_sgd_chains_fed(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
     const uint32_t* __restrict__ ent, int ns, float eta32, double eta64) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ uint32_t ctl[8];
+    __shared__ uint32_t ctl[kFedCtl];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t items = counters[kCntM] * (uint32_t)ns;
     __builtin_amdgcn_s_setprio(3);
     for (;;) {
         if (threadIdx.x == 0) {
-            fed_set(ctl, 0, 0u);
-            fed_set(ctl, 1, 0u);
-            fed_set(ctl, 2, 0u);
-            fed_set(ctl, kFedFree, 0u);
+            for (int k = 0; k < kFedGather + 1; ++k) fed_set(ctl, k, 0u);
             fed_set(ctl, kFedItem, atomicAdd(&counters[kCntNext], 1u));
         }
         __syncthreads();
@@ -2259,13 +2225,14 @@ __global__ __launch_bounds__(256) void k_sgd_chains_fed(
         const int t = table_of_key(pack, ntables, c.key);
         const et_update_desc& d = pack.d[t];
         const uint32_t nch = c.ngr;
+        float* row = lds + lane * kFedPitch;
         if (c.S != 0u && slice * 64 < d.dim && nch > 0u) {  // workgroup-uniform
             if (wave == 0) {  // the serial sum
                 float acc = 0.0f;
-                const float* row = lds + lane * kFedPitch;
                 for (uint32_t ch = 0; ch < nch; ++ch) {
-                    const uint32_t need = ch / 3u + 1u;
-                    while (fed_get(ctl, (int)(ch % 3u)) < need) __builtin_amdgcn_s_sleep(0);
+                    const uint32_t need = ch / (uint32_t)kFedGather + 1u;
+                    while (fed_get(ctl, (int)(ch % (uint32_t)kFedGather)) < need)
+                        __builtin_amdgcn_s_sleep(0);
                     __atomic_signal_fence(__ATOMIC_SEQ_CST);
                     const f32x4* src = reinterpret_cast<const f32x4*>(
                         row + (int)(ch % (uint32_t)(kFedSlots / 64)) * 64);
@@ -2288,45 +2255,28 @@ __global__ __launch_bounds__(256) void k_sgd_chains_fed(
                                               c.key - pack.row_off[t]) + f;
                     store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
                 }
-            } else {  // gatherer p: chunks p, p + 3, ...
-                const int p = wave - 1;
+            } else {  // gatherer p: chunks p, p + 7, ... (et_chain_asm.h, fed_gather_asm)
+                static_assert(kFedAsmGatherers == kFedGather && kFedFree == kFedGather &&
+                                  kFedSlots == 512, "fed gatherer layout (tools/gen_chain_asm.py)");
+                const uint32_t p = (uint32_t)(wave - 1);
                 const uint32_t ld = (uint32_t)d.ld_delta;
-                const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<void*>(d.delta), 0, (int)((uint32_t)d.batch * ld * 4u), 0x00020000);
-                const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint32_t*>(ent + c.e0), 0, (int)(nch * 256u), 0x00020000);
-                // lane 16q + i loads entry 4i + q of a chunk (row_newbcast:k -> entry 4k + q)
-                const uint32_t poff = 4u * (4u * (uint32_t)(lane & 15) + (uint32_t)(lane >> 4));
-                const uint32_t fbyte = 4u * (uint32_t)(slice * 64 + 4 * (lane & 15));
-                const uint32_t ld4 = 4u * ld;
-                // this gatherer's chunks: i = 0, 1, .. is chunk p + 3i.  Issue order per
-                // step i: entries of chunk i+3, put chunk i (waits for its rows), rows of
-                // chunk i+2 into the freed buffer — so the entries a row load needs were
-                // issued before the previous chunk's rows and never drain them (loads
-                // complete in order); two row buffers and two entry registers alternate
-                // by step parity (no copies of registers with loads in flight)
-                const uint32_t nm = (uint32_t)p < nch ? (nch - (uint32_t)p + 2u) / 3u : 0u;
-                // unconditional: a chunk past the list is past the entries' range (loads 0)
-                auto entries = [&](uint32_t i) {
-                    return __builtin_amdgcn_raw_buffer_load_b32(
-                        re, (int)(((uint32_t)p + 3u * i) * 256u + poff), 0, 0);
-                };
-                f32x4 xa[16], xb[16];
-                const uint32_t e0v = entries(0u), e1v = entries(1u);
-                fed_issue<0>(xa, e0v, rx, ld4, fbyte);
-                fed_issue<0>(xb, e1v, rx, ld4, fbyte);
-                uint32_t ra = entries(2u), rb = 0u;
-                // the row loads are unconditional (past the list the entries load 0: row 0,
-                // never put), so every pending load is consumed on every path and the
-                // compiler's wait counts stay partial across the loop's back edge
-                for (uint32_t i = 0; i < nm; i += 2u) {
-                    fed_put(xa, lds, ctl, (uint32_t)p + 3u * i, p, lane);
-                    rb = entries(i + 3u);
-                    fed_issue<0>(xa, ra, rx, ld4, fbyte);
-                    if (i + 1u >= nm) break;
-                    fed_put(xb, lds, ctl, (uint32_t)p + 3u * (i + 1u), p, lane);
-                    ra = entries(i + 4u);
-                    fed_issue<0>(xb, rb, rx, ld4, fbyte);
+                const uint32_t nm =
+                    p < nch ? (nch - p + (uint32_t)kFedGather - 1u) / (uint32_t)kFedGather : 0u;
+                if (nm > 0u) {
+                    const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
+                    const float* delta = reinterpret_cast<const float*>(
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
+                    const uint64_t eb = reinterpret_cast<uint64_t>(ent + c.e0);
+                    const float* ep = reinterpret_cast<const float*>(
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)eb) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(eb >> 32)) << 32);
+                    const i32x4 rx = chain_rsrc(delta, (uint32_t)d.batch * ld * 4u);
+                    const i32x4 re = chain_rsrc(ep, nch * 256u);
+                    const uint32_t rowa = (uint32_t)reinterpret_cast<uintptr_t>(row);
+                    const uint32_t ctla = (uint32_t)reinterpret_cast<uintptr_t>(&ctl[0]);
+                    fed_gather_asm(nm, p, re, rx, 4u * (uint32_t)(slice * 64 + lane),
+                                   4u * (uint32_t)lane, 4u * ld, rowa, ctla, ctla + 4u * p);
                 }
             }
         }
@@ -2569,6 +2519,43 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
     return (P & 1) ? Grouped{w.kb, w.vb} : Grouped{w.ka, w.va};
 }
 
+// Exact Float32 mode: the multi-chunk columns become serial chains.  Their plan reads only
+// the index phase's segments and multi-chunk list, so it runs on the regular chains' side
+// stream (forked after the chunk records) while the caller's stream goes on to the chunk pass
+// over the single-chunk columns (k_sgd_exact) — the plan is off the update's critical path.
+inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
+                             uint32_t chunk, UpdateWs& w, const Grouped& out, hipStream_t s,
+                             uint32_t ec_mask) {
+    const int64_t mmax = n / chunk + 2;
+    const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
+    const int64_t tmax = chain_tiles_max(n, chunk);
+    const unsigned tg = (unsigned)(tmax < 8192 ? tmax : 8192);
+    hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask,
+                       out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
+                       w.chain_tile_col);
+    hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                       out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                       w.chain_tile_col, w.chain_tcnt);
+    hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
+                       w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
+                       w.chain_info, w.chains, chain_fed(false) ? 0 : 4);
+    hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
+                       w.chain_info, w.chain_e0, w.chain_order);
+    hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                       out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                       w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
+                       w.chain_ent, w.chains);
+    ET_LAUNCH_CHECK("k_chain_emit");
+    static const bool check = [] {
+        const char* e = getenv("ET_CHAIN_CHECK");
+        return e && atoi(e) != 0;
+    }();
+    if (check)
+        hipLaunchKernelGGL(k_chain_check, dim3(cg), dim3(256), 0, s, pack, ntables, w.counters,
+                           w.chain_cnt, w.chain_info, w.chain_ent, w.chains, w.chain_order);
+    return ET_OK;
+}
+
 inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, Grouped& out, hipStream_t s,
                              uint32_t hot_mask = 0, const HotList* hl = nullptr,
@@ -2638,35 +2625,6 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chunk_records_multi, dim3(512), dim3(256), 0, s, w.nch, w.seg_start,
                        w.multi, out.keys, w.mlist, chunk, w.counters, w.recs);
     ET_LAUNCH_CHECK("k_chunk_records");
-    if (chain) {  // exact Float32 mode: the multi-chunk columns become serial chains
-        const int64_t mmax = n / chunk + 2;
-        const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
-        const int64_t tmax = chain_tiles_max(n, chunk);
-        const unsigned tg = (unsigned)(tmax < 8192 ? tmax : 8192);
-        hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask,
-                           out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
-                           w.chain_tile_col);
-        hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
-                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                           w.chain_tile_col, w.chain_tcnt);
-        hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
-                           w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
-                           w.chain_info, w.chains, chain_fed() ? 0 : 4);
-        hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
-                           w.chain_info, w.chain_e0, w.chain_order);
-        hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
-                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                           w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
-                           w.chain_ent, w.chains);
-        ET_LAUNCH_CHECK("k_chain_emit");
-        static const bool check = [] {
-            const char* e = getenv("ET_CHAIN_CHECK");
-            return e && atoi(e) != 0;
-        }();
-        if (check)
-            hipLaunchKernelGGL(k_chain_check, dim3(cg), dim3(256), 0, s, pack, ntables, w.counters,
-                               w.chain_cnt, w.chain_info, w.chain_ent, w.chains, w.chain_order);
-    }
     if (hot_mask && w.hot_hist && hl && hl->n > 0) {
         ET_HIP_CHECK(hipMemsetAsync(w.hot_hist, 0, 4 * (32 * 32 + 32), s));
         hipLaunchKernelGGL(k_hot_hist, dim3(256), dim3(256), 0, s, pack, ntables, hot_mask,
@@ -2742,7 +2700,7 @@ template <int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
                   const uint32_t* order, const uint2* info, const uint32_t* nocc,
                   const uint32_t* ent, int ns, float eta32, double eta64, unsigned nhf,
-                  unsigned nb, hipStream_t s, bool excl = false) {
+                  unsigned nb, hipStream_t s, bool excl = false, bool fed = false) {
     static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++;
         // experiments: ET_CHAIN_QUAD=0 walks S = 1 chains with the 64-feature asm loop
         const char* e = getenv("ET_CHAIN_ASM");
@@ -2775,12 +2733,13 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
     else
         ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
     ET_HIP_CHECK(hipMemsetAsync(counters + kCntHfNext, 0, 4, s));
-    if (chain_fed()) {  // every chain planned at S = 1: the fed walk
+    if (fed) {  // every chain planned at S = 1: the fed walk
         static const hipError_t attr_f = hipFuncSetAttribute(
             reinterpret_cast<const void*>(&k_sgd_chains_fed<MODE, NT>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFedLds);
         ET_HIP_CHECK(attr_f);
-        hipLaunchKernelGGL((k_sgd_chains_fed<MODE, NT>), dim3(nb), dim3(256), kFedLds, s, pack,
+        hipLaunchKernelGGL((k_sgd_chains_fed<MODE, NT>), dim3(nb), dim3(64 * (kFedGather + 1)),
+                           kFedLds, s, pack,
                            ntables, counters, chains, order, ent, ns, eta32, eta64);
         ET_LAUNCH_CHECK("k_sgd_chains_fed");
         return ET_OK;
@@ -2833,12 +2792,12 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         const unsigned hf_wg = 0u;
         rc = launch_chains<MODE, NT>(pack, ntables, w.ec_counters, w.ec_chains, w.ec_order,
                                      w.ec_info, w.ec_nocc, w.ec_ent, ns, eta32, eta64, hf_wg, eb,
-                                     cr.ec_side, (excl & 1u) != 0);
+                                     cr.ec_side, (excl & 1u) != 0, chain_fed(true));
         if (rc != ET_OK) return rc;
     }
     rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
                                  w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u, reg_wg,
-                                 cr.side, (excl & 2u) != 0);
+                                 cr.side, (excl & 2u) != 0, chain_fed(false));
     if (rc != ET_OK) return rc;
 #define ET_SGD_EXACT(DD)                                                                       \
     case DD:                                                                                   \
@@ -3158,7 +3117,7 @@ inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chu
     hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_stats);
     hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
                        w.ec_stats, w.ec_boff, w.ec_cnt, w.ec_nocc, w.ec_info, w.ec_chains,
-                       w.ec_ent, w.ec_counters, chain_fed() ? 0 : 4);
+                       w.ec_ent, w.ec_counters, chain_fed(true) ? 0 : 4);
     hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.ec_info, w.ec_nocc, ns,
                        w.ec_order, w.ec_counters);
     hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_boff,
@@ -3327,15 +3286,21 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     } else {
         rc = et::group_occurrences(pack, ntables, n, sent, chunk, w, gr, s, hot_mask, &hl, chain,
                                    use_ec ? ec.mask : 0u, snaps);
-        if (rc != ET_OK || index_only) return rc;
+        if (rc != ET_OK) return rc;
     }
     et::ChainRun cr;
     if (chain) {
         cr.ec_side = ec_side;
         cr.ec_ncols = use_ec ? ec.col0[ec.n] : 0u;
-        cr.side = fork.fork(1);  // after the index phase
+        cr.side = fork.fork(1);  // after the index phase's chunk records
         if (!cr.side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
+        if (!apply_only) {
+            rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, cr.side,
+                                       use_ec ? ec.mask : 0u);
+            if (rc != ET_OK) return rc;
+        }
     }
+    if (index_only) return ET_OK;
 
     const bool nt = (flags & ET_FLAG_NONTEMPORAL) != 0;
     const int mode = (flags & ET_FLAG_SGD_UNFUSED) ? ((flags & ET_FLAG_SGD_F64_ALPHA) ? 2 : 1) : 0;

@@ -18,3 +18,10 @@ ET_CHAIN_FED=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -
   -- python3 tools/exact_cfg4.py exact > $OUT/exact_traced.txt 2>&1 || { echo TRACE_FAIL; tail -5 $OUT/exact_traced.txt; exit 1; }
 f=$(ls $OUT/prof/*/run_kernel_trace.csv $OUT/prof/run_kernel_trace.csv 2>/dev/null | head -1)
 python3 tools/upd_timeline.py "$f" > $OUT/exact_timeline.txt && grep -E "chains|sgd_exact|total" $OUT/exact_timeline.txt
+# 256-byte rows on the scalar-addressed loop (ET_SG256=1): lookup parity, fp16 leg A/B
+ET_SG256=1 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_lookup.py -x -q -m gpu --timeout 200 --timeout-method thread > $OUT/pytest_sg256.log 2>&1 || { echo SG256_TEST_FAIL; tail -30 $OUT/pytest_sg256.log; exit 1; }
+tail -1 $OUT/pytest_sg256.log
+for i in 1 2; do for v in 0 1; do
+  ET_SG256=$v timeout -k 10 200 python3 tools/fp16_leg.py > $OUT/fp16_${v}_$i.txt 2>&1 || { echo FP16_FAIL; tail -5 $OUT/fp16_${v}_$i.txt; exit 1; }
+  echo "SG256=$v $(python3 -c "import json,sys; d=json.loads(open('$OUT/fp16_${v}_$i.txt').read().strip().splitlines()[-1]); print(round(d['julia_f16_arith']['kernel_ms'],4), round(d['fp32_accumulate']['kernel_ms'],4))")"
+done; done
