@@ -1335,9 +1335,14 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
             continue;
         }
         uint32_t E[5] = {0u, 0u, 0u, 0u, 0u};
-        for (uint32_t i = (uint32_t)lane; i < nt; i += 64)
+        if (tcnt) {
+            for (uint32_t i = (uint32_t)lane; i < nt; i += 64)
 #pragma unroll
-            for (int k = 0; k < 5; ++k) E[k] += tcnt[5 * (t0 + i) + k];
+                for (int k = 0; k < 5; ++k) E[k] += tcnt[5 * (t0 + i) + k];
+        } else if (lane == 0) {  // S = 1 only (fed chains): one entry per occurrence
+            const uint32_t u = mlist[m];
+            E[0] = seg_start[u + 1] - seg_start[u];
+        }
         int best = 0;
         uint64_t bc = ~0ull;
 #pragma unroll
@@ -1473,6 +1478,41 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
                 chains[c.m] = ChainCol{keys[c.ss], e0, (P - kChainPad) / kChainGroup, S};
         }
         __syncthreads();  // bags, rl and red are reused by the next tile
+    }
+}
+
+// Index phase 5 for S = 1 plans (fed chains): every occurrence is one entry (r = 1) of its
+// gradient column, in occurrence order — a copy of the sorted pairs' bags; the column's last
+// tile pads to the planned count (bag = batch: loads +0) and writes the descriptor.
+__global__ __launch_bounds__(256) void k_chain_emit1(UpdatePack pack, int ntables,
+                                                     const uint32_t* __restrict__ keys,
+                                                     const uint32_t* __restrict__ vals,
+                                                     const uint32_t* __restrict__ seg_start,
+                                                     const uint32_t* __restrict__ mlist,
+                                                     const uint32_t* __restrict__ counters,
+                                                     const uint32_t* __restrict__ tile0,
+                                                     const uint32_t* __restrict__ tile_col,
+                                                     const uint32_t* __restrict__ cnt,
+                                                     const uint2* __restrict__ info,
+                                                     const uint32_t* __restrict__ e0s,
+                                                     uint32_t* __restrict__ ent,
+                                                     ChainCol* __restrict__ chains) {
+    const uint32_t M = counters[kCntM], T = counters[kCntT];
+    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
+        const ChainTile c = chain_tile(pack, ntables, keys, seg_start, mlist, tile0, tile_col, M,
+                                       T, tile);
+        const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
+        const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
+        const uint32_t e0 = e0s[c.m], at = e0 + (c.a - c.ss);
+        for (uint32_t i = threadIdx.x; i < n; i += 256)
+            ent[at + i] = chain_entry(1u, (vals[c.a + i] - occ_off) / pool);
+        if (c.ti + 1 == c.nt) {
+            const uint32_t P = cnt[c.m];
+            const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[c.t].batch);
+            for (uint32_t i = e0 + info[c.m].y + threadIdx.x; i < e0 + P; i += 256) ent[i] = pad;
+            if (threadIdx.x == 0)
+                chains[c.m] = ChainCol{keys[c.ss], e0, (P - kChainPad) / kChainGroup, 1u};
+        }
     }
 }
 
@@ -2533,18 +2573,26 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask,
                        out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
                        w.chain_tile_col);
-    hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
-                       out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                       w.chain_tile_col, w.chain_tcnt);
+    const bool s1 = chain_fed(false);  // S = 1 plans: entries = occurrences, no run counts
+    if (!s1)
+        hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                           w.chain_tile_col, w.chain_tcnt);
     hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
-                       w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
-                       w.chain_info, w.chains, chain_fed(false) ? 0 : 4);
+                       w.mlist, w.counters, w.chain_tile0, s1 ? nullptr : w.chain_tcnt,
+                       w.chain_cnt, w.chain_info, w.chains, s1 ? 0 : 4);
     hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
                        w.chain_info, w.chain_e0, w.chain_order);
-    hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
-                       out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                       w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
-                       w.chain_ent, w.chains);
+    if (s1)
+        hipLaunchKernelGGL(k_chain_emit1, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                           w.chain_tile_col, w.chain_cnt, w.chain_info, w.chain_e0, w.chain_ent,
+                           w.chains);
+    else
+        hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                           w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
+                           w.chain_ent, w.chains);
     ET_LAUNCH_CHECK("k_chain_emit");
     static const bool check = [] {
         const char* e = getenv("ET_CHAIN_CHECK");
@@ -3292,9 +3340,21 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     if (chain) {
         cr.ec_side = ec_side;
         cr.ec_ncols = use_ec ? ec.col0[ec.n] : 0u;
-        cr.side = fork.fork(1);  // after the index phase's chunk records
+        // the regular chains' plan: on their side stream beside the chunk pass (default), or
+        // on the caller's stream before it (ET_PLAN_SIDE=0: the chains start earlier, the
+        // chunk pass later)
+        static const bool plan_side = [] {
+            const char* e = getenv("ET_PLAN_SIDE");
+            return e ? atoi(e) != 0 : true;
+        }();
+        if (!apply_only && !plan_side) {
+            rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, s,
+                                       use_ec ? ec.mask : 0u);
+            if (rc != ET_OK) return rc;
+        }
+        cr.side = fork.fork(1);  // after the index phase's chunk records (and the plan)
         if (!cr.side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
-        if (!apply_only) {
+        if (!apply_only && plan_side) {
             rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, cr.side,
                                        use_ec ? ec.mask : 0u);
             if (rc != ET_OK) return rc;

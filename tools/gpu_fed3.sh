@@ -17,3 +17,7 @@ ET_CHAIN_FED=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof$
 f=$(ls $OUT/prof$v/*/run_kernel_trace.csv $OUT/prof$v/run_kernel_trace.csv 2>/dev/null | head -1)
 python3 tools/upd_timeline.py "$f" > $OUT/exact_timeline$v.txt && echo "timeline fed=$v" && grep -E "chains|sgd_exact|total" $OUT/exact_timeline$v.txt
 done
+for v in "ET_PLAN_SIDE=0" "ET_PLAN_SIDE=0 ET_CHAIN_FED=2" "ET_PLAN_SIDE=0 ET_CHAIN_FED=1"; do
+  env $v timeout -k 10 200 python3 tools/exact_cfg4.py exact > $OUT/cfg4_ps.txt 2>&1 || { echo CFG4_FAIL $v; tail -5 $OUT/cfg4_ps.txt; exit 1; }
+  echo "$v $(tail -1 $OUT/cfg4_ps.txt)"
+done
