@@ -1232,12 +1232,33 @@ __device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32
     return v + off;
 }
 
+// The early hot-column candidates of the big tables (ET_EH, see EcList below): kEhK
+// ascending columns per table, ~0 past the last; EhMap says which tables have a list and
+// where it is.
+constexpr int kEhK = 64;  // candidate columns per table
+struct EhMap {
+    uint32_t mask;                      // bit t: table t has a candidate list
+    int8_t e[ET_MAX_TABLES_PER_LAUNCH];  // its entry: the list at cand + e * kEhK
+};
+
+// Slot of column c in a table's ascending candidate list (kEhK entries, ~0 = empty), or -1.
+__device__ __forceinline__ int eh_slot(const uint32_t* cand, uint32_t c) {
+    int lo = 0, hi = kEhK;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cand[mid] < c) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < kEhK && cand[lo] == c ? lo : -1;
+}
+
 // Index phase 1 (one workgroup): tiles per chain column (none for the out-of-range
-// sentinel column, nor for the columns of early-chain tables, ec_mask: those chains are
-// planned from the index arrays, k_ec_*), the first tile of each column, the tile ->
-// column map and the tile total (counters[kCntT]).
+// sentinel column, nor for the columns of early-chain tables, ec_mask, nor for the
+// early hot-column candidates, eh: those chains are planned from the index arrays, k_ec_*),
+// the first tile of each column, the tile -> column map and the tile total (counters[kCntT]).
 __global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntables,
-                                                      uint32_t ec_mask,
+                                                      uint32_t ec_mask, EhMap eh,
+                                                      const uint32_t* __restrict__ cand,
                                                       const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ seg_start,
                                                       const uint32_t* __restrict__ mlist,
@@ -1253,8 +1274,11 @@ __global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntabl
         if (m < M) {
             const uint32_t u = mlist[m], ss = seg_start[u], se = seg_start[u + 1];
             const uint32_t k0 = keys[ss];
-            v = k0 == sent || ((ec_mask >> table_of_key(pack, ntables, k0)) & 1u)
-                    ? 0u : cdiv_u32(se - ss, kChainTile);
+            const int t = k0 == sent ? 0 : table_of_key(pack, ntables, k0);
+            const bool early = k0 == sent || ((ec_mask >> t) & 1u) ||
+                               (((eh.mask >> t) & 1u) &&
+                                eh_slot(cand + eh.e[t] * kEhK, k0 - pack.row_off[t]) >= 0);
+            v = early ? 0u : cdiv_u32(se - ss, kChainTile);
         }
         uint32_t total;
         const uint32_t inc = block_inclusive_scan_1024(v, lds16, &total);
@@ -1575,13 +1599,28 @@ constexpr int kEcMaxBatch = 1 << 20;
 constexpr int kEcStats = 8;      // per (column, block): occurrences, entries at S = 1..16
 constexpr uint32_t kHfMinOcc = 65536;  // helper-fed chains: at least this many occurrences
 
+// Early HOT columns of the larger tables (round 4, ET_EH): every table of more than
+// kEcMaxRows rows gets kEhK "slots" — the columns a sample of its first kEhSampleBags bags
+// finds hottest (k_eh_pick: at least kEhMinOcc occurrences expected over the batch, at most
+// kEhK per table, ascending column order) — planned as early chains of their own (a second
+// EcList, hot = 1, on a third side stream), so the big tables' longest chains start with
+// the call instead of after the sort.  The slots are counted, planned and emitted by the
+// same k_ec_* kernels (a bag's indices are matched against the table's candidate list); a
+// candidate with more than `chunk` occurrences is a chain there, and the regular plan skips
+// it (k_chain_tiles), so every column is summed exactly once.
+constexpr int kEhSampleBags = 4096;     // bags sampled by k_eh_pick
+constexpr uint32_t kEhMinOcc = 4096;    // expected occurrences of a candidate
+constexpr int kEhHash = 4096;           // LDS hash slots of the sample count
+constexpr int kEhProbes = 16;           // linear probes per occurrence
+
 struct EcList {
     int n;                                        // early-chain tables
     uint32_t mask;                                // bit t: table t is one of them
+    int hot;                                      // 1: kEhK candidate slots per table (EH)
     int t[ET_MAX_TABLES_PER_LAUNCH];              // their table indices
     uint32_t blk0[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of bag blocks
-    uint32_t col0[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of nrows (EC columns)
-    uint32_t cb0[ET_MAX_TABLES_PER_LAUNCH + 1];   // prefix of blocks x nrows (stat records)
+    uint32_t col0[ET_MAX_TABLES_PER_LAUNCH + 1];  // prefix of nrows / kEhK (EC columns)
+    uint32_t cb0[ET_MAX_TABLES_PER_LAUNCH + 1];   // prefix of blocks x columns (stat records)
 };
 
 inline bool ec_table(const et_update_desc& d) {
@@ -1589,11 +1628,82 @@ inline bool ec_table(const et_update_desc& d) {
            d.batch > 0 && d.batch <= kEcMaxBatch && d.dim > 0;
 }
 
+inline bool eh_table(const et_update_desc& d) {
+    return d.nrows > kEcMaxRows && d.nrows < (1ll << 31) && d.pool > 0 &&
+           d.pool <= kEcMaxPool && d.batch > 0 && d.batch <= kEcMaxBatch && d.dim > 0;
+}
+
+inline bool eh_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("ET_EH");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
+// One workgroup per EH entry: count the sampled bags' columns in an LDS hash table, keep the
+// columns expected to reach kEhMinOcc occurrences, at most kEhK of them (the most frequent;
+// ties to the smaller column), and write them in ascending order, ~0 past the last.
+__global__ __launch_bounds__(1024) void k_eh_pick(UpdatePack pack, EcList ec, uint32_t min_occ,
+                                                  uint32_t* __restrict__ cand) {
+    __shared__ uint32_t hk[kEhHash], hc[kEhHash];
+    __shared__ uint32_t qk[512], qc[512], nq;
+    __shared__ uint32_t sel[kEhK], nsel;
+    const int e = blockIdx.x;
+    const et_update_desc& d = pack.d[ec.t[e]];
+    for (int i = threadIdx.x; i < kEhHash; i += 1024) hk[i] = ~0u, hc[i] = 0u;
+    if (threadIdx.x == 0) nq = 0u, nsel = 0u;
+    __syncthreads();
+    const int64_t nb = d.batch < kEhSampleBags ? d.batch : kEhSampleBags;
+    const int64_t nocc = nb * d.pool;
+    for (int64_t o = threadIdx.x; o < nocc; o += 1024) {
+        const int64_t b = o / d.pool, j = o - b * d.pool;
+        const uint64_t c = (uint64_t)(d.idx[b * d.ld_idx + j] - 1);
+        if (c >= (uint64_t)d.nrows) continue;
+        uint32_t h = ((uint32_t)c * 2654435761u) >> 20;  // 12 bits
+        for (int probe = 0; probe < kEhProbes; ++probe, h = (h + 1) & (kEhHash - 1)) {
+            const uint32_t prev = atomicCAS(&hk[h], ~0u, (uint32_t)c);
+            if (prev == ~0u || prev == (uint32_t)c) {
+                atomicAdd(&hc[h], 1u);
+                break;
+            }
+        }  // a crowded neighbourhood drops the occurrence: the sample only ranks columns
+    }
+    __syncthreads();
+    // expected total >= min_occ  <=>  sample count * batch >= min_occ * nb
+    for (int i = threadIdx.x; i < kEhHash; i += 1024)
+        if (hk[i] != ~0u && (uint64_t)hc[i] * (uint64_t)d.batch >= (uint64_t)min_occ * (uint64_t)nb) {
+            const uint32_t q = atomicAdd(&nq, 1u);
+            if (q < 512) qk[q] = hk[i], qc[q] = hc[i];
+        }
+    __syncthreads();
+    const uint32_t Q = nq < 512 ? nq : 512u;
+    if (threadIdx.x < Q) {  // rank by (count desc, column asc)
+        const uint32_t k = qk[threadIdx.x], n = qc[threadIdx.x];
+        uint32_t r = 0;
+        for (uint32_t i = 0; i < Q; ++i) r += qc[i] > n || (qc[i] == n && qk[i] < k);
+        if (r < (uint32_t)kEhK) sel[atomicAdd(&nsel, 1u)] = k;
+    }
+    __syncthreads();
+    const uint32_t S = nsel;
+    if (threadIdx.x < kEhK) {  // ascending column order
+        uint32_t v = ~0u;
+        if (threadIdx.x < S) {
+            const uint32_t k = sel[threadIdx.x];
+            uint32_t r = 0;
+            for (uint32_t i = 0; i < S; ++i) r += sel[i] < k;
+            v = k;
+            cand[e * kEhK + r] = v;
+        }
+        if (threadIdx.x >= S) cand[e * kEhK + threadIdx.x] = ~0u;
+    }
+}
+
 // Per-bag column counts in LDS: row `tid` (bag blk * kEcBags + tid) holds r(c, bag) for
 // the table's R <= kEcMaxRows columns, one byte each (out-of-range indices are not
 // counted; the main index phase reports them).
 __device__ __forceinline__ void ec_hist(const et_update_desc& d, uint32_t blk, uint8_t* hist,
-                                        uint32_t RS) {
+                                        uint32_t RS, const uint32_t* cand = nullptr) {
     const uint32_t R = (uint32_t)d.nrows, pool = (uint32_t)d.pool;
     uint32_t* row = reinterpret_cast<uint32_t*>(hist + threadIdx.x * RS);
     for (uint32_t i = 0; i < RS / 4; ++i) row[i] = 0u;
@@ -1603,10 +1713,22 @@ __device__ __forceinline__ void ec_hist(const et_update_desc& d, uint32_t blk, u
         uint8_t* h = hist + threadIdx.x * RS;
         for (uint32_t j = 0; j < pool; ++j) {
             const uint64_t c = (uint64_t)(ip[j] - 1);
-            if (c < R) h[c] = (uint8_t)(h[c] + 1u);
+            if (c >= R) continue;
+            const int slot = cand ? eh_slot(cand, (uint32_t)c) : (int)c;  // EH: candidates only
+            if (slot >= 0) h[slot] = (uint8_t)(h[slot] + 1u);
         }
     }
     __syncthreads();
+}
+
+// An EH entry's candidate list in LDS (the k_ec_* kernels' slot map), or nullptr.
+__device__ __forceinline__ const uint32_t* eh_stage(const EcList& ec, int e,
+                                                    const uint32_t* __restrict__ cand,
+                                                    uint32_t* lds) {
+    if (!ec.hot) return nullptr;
+    if (threadIdx.x < kEhK) lds[threadIdx.x] = cand[e * kEhK + threadIdx.x];
+    __syncthreads();
+    return lds;
 }
 
 __device__ __forceinline__ int ec_find(const EcList& ec, uint32_t blk) {
@@ -1640,15 +1762,17 @@ __device__ __forceinline__ EcParts ec_parts(uint32_t R) {
 // EC step 1, one workgroup per (table, block of kEcBags bags): per column, its occurrences
 // in the block and the entries they make at S = 1, 2, 4, 8, 16.
 __global__ __launch_bounds__(256) void k_ec_count(UpdatePack pack, EcList ec,
-                                                  uint32_t* __restrict__ stats) {
+                                                  uint32_t* __restrict__ stats,
+                                                  const uint32_t* __restrict__ cand) {
     __shared__ __attribute__((aligned(16))) uint8_t hist[kEcBags * kEcMaxRows];
     __shared__ uint32_t red[kEcBags][6];
+    __shared__ uint32_t sc[kEhK];
     const int e = ec_find(ec, blockIdx.x);
     const et_update_desc& d = pack.d[ec.t[e]];
     const uint32_t blk = blockIdx.x - ec.blk0[e];
     const uint32_t nblk = ec.blk0[e + 1] - ec.blk0[e];
-    const EcParts q = ec_parts((uint32_t)d.nrows);
-    ec_hist(d, blk, hist, q.RS);
+    const EcParts q = ec_parts(ec.col0[e + 1] - ec.col0[e]);
+    ec_hist(d, blk, hist, q.RS, eh_stage(ec, e, cand, sc));
     uint32_t v[6] = {0u, 0u, 0u, 0u, 0u, 0u};
     for (uint32_t i = q.b0; i < q.b1; ++i) {
         const uint32_t r = hist[i * q.RS + q.c];
@@ -1682,7 +1806,8 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
                                                  uint2* __restrict__ info,
                                                  ChainCol* __restrict__ chains,
                                                  uint32_t* __restrict__ ent,
-                                                 uint32_t* __restrict__ counters, int kmax) {
+                                                 uint32_t* __restrict__ counters, int kmax,
+                                                 const uint32_t* __restrict__ cand) {
     const int lane = threadIdx.x & 63;
     const uint32_t M = ec.col0[ec.n];
     const uint32_t g = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -1716,8 +1841,9 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
         cnt[g] = P;
         nocc[g] = v[0];
         info[g] = make_uint2(S, E);
-        chains[g] = ChainCol{pack.row_off[t] + c, e0, is_chain ? (P - kChainPad) / kChainGroup : 0u,
-                             S};
+        const uint32_t col = ec.hot ? cand[e * kEhK + c] : c;  // EH: the candidate
+        chains[g] = ChainCol{is_chain ? pack.row_off[t] + col : 0u, e0,
+                             is_chain ? (P - kChainPad) / kChainGroup : 0u, S};
     }
     if (!is_chain) return;
     uint32_t carry = e0;  // per-block entry offsets at S, in block order
@@ -1771,15 +1897,17 @@ __global__ __launch_bounds__(1024) void k_ec_order(EcList ec, const uint2* __res
 __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
                                                  const uint32_t* __restrict__ boff,
                                                  const uint2* __restrict__ info,
-                                                 uint32_t* __restrict__ ent) {
+                                                 uint32_t* __restrict__ ent,
+                                                 const uint32_t* __restrict__ cand) {
     __shared__ __attribute__((aligned(16))) uint8_t hist[kEcBags * kEcMaxRows];
     __shared__ uint32_t psum[kEcBags];
+    __shared__ uint32_t sc[kEhK];
     const int e = ec_find(ec, blockIdx.x);
     const et_update_desc& d = pack.d[ec.t[e]];
     const uint32_t blk = blockIdx.x - ec.blk0[e];
     const uint32_t nblk = ec.blk0[e + 1] - ec.blk0[e];
-    const EcParts q = ec_parts((uint32_t)d.nrows);
-    ec_hist(d, blk, hist, q.RS);
+    const EcParts q = ec_parts(ec.col0[e + 1] - ec.col0[e]);
+    ec_hist(d, blk, hist, q.RS, eh_stage(ec, e, cand, sc));
     const uint32_t S = q.on ? info[ec.col0[e] + q.c].x : 0u;
     uint32_t mine = 0;
     if (S)
@@ -2443,9 +2571,13 @@ struct UpdateWs {
     // early chains (EcList): per (column, block) stats and entry offsets, per EC column the
     // padded entry count, (S, entries), descriptor and cost order, their entries, and a
     // counter block (kCntM = EC columns) for the chain role
-    uint32_t *ec_stats, *ec_boff, *ec_cnt, *ec_order, *ec_ent, *ec_counters, *ec_nocc;
-    uint2* ec_info;
-    ChainCol* ec_chains;
+    struct EcWs {
+        uint32_t *stats, *boff, *cnt, *order, *ent, *counters, *nocc;
+        uint2* info;
+        ChainCol* chains;
+    };
+    EcWs ec, eh;        // the small tables' early chains; the big tables' hot columns (ET_EH)
+    uint32_t* eh_cand;  // kEhK candidate columns per EH entry (k_eh_pick)
     int64_t bytes;
 };
 
@@ -2461,7 +2593,8 @@ inline int64_t chain_tiles_max(int64_t n, uint32_t chunk) {
 // partial rows of pdim floats.
 inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
                                 int nhot = 0, int64_t hot_batch = 0, int64_t hot_bytes = 0,
-                                const EcList* ec = nullptr, int64_t ec_occ = 0) {
+                                const EcList* ec = nullptr, int64_t ec_occ = 0,
+                                const EcList* eh = nullptr, int64_t eh_occ = 0) {
     UpdateWs w;
     // every buffer 256-byte aligned whatever the caller's workspace alignment (the
     // 16-byte key / index / LDS-DMA loads rely on it): the layout starts at the first
@@ -2505,18 +2638,23 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
     w.chain_tile0 = (uint32_t*)take(4 * mmax);
     w.chain_tile_col = (uint32_t*)take(4 * tmax);
     w.chain_tcnt = (uint32_t*)take(20 * tmax);
-    {
-        const int64_t recs = ec && ec->n ? ec->cb0[ec->n] : 0, M = ec && ec->n ? ec->col0[ec->n] : 0;
-        w.ec_stats = (uint32_t*)take(4 * kEcStats * recs);
-        w.ec_boff = (uint32_t*)take(4 * recs);
-        w.ec_cnt = (uint32_t*)take(4 * M);
-        w.ec_order = (uint32_t*)take(4 * M);
-        w.ec_nocc = (uint32_t*)take(4 * M);
-        w.ec_info = (uint2*)take(8 * M);
-        w.ec_chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * M);
-        w.ec_counters = (uint32_t*)take(4 * kCntSlots);
-        w.ec_ent = (uint32_t*)take(4 * (ec_occ + (int64_t)(kChainGroup + kChainPad) * M + 64));
-    }
+    auto carve_ec = [&](const EcList* l, int64_t occ) {
+        const int64_t recs = l && l->n ? l->cb0[l->n] : 0, M = l && l->n ? l->col0[l->n] : 0;
+        UpdateWs::EcWs e;
+        e.stats = (uint32_t*)take(4 * kEcStats * recs);
+        e.boff = (uint32_t*)take(4 * recs);
+        e.cnt = (uint32_t*)take(4 * M);
+        e.order = (uint32_t*)take(4 * M);
+        e.nocc = (uint32_t*)take(4 * M);
+        e.info = (uint2*)take(8 * M);
+        e.chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * M);
+        e.counters = (uint32_t*)take(4 * kCntSlots);
+        e.ent = (uint32_t*)take(4 * (occ + (int64_t)(kChainGroup + kChainPad) * M + 64));
+        return e;
+    };
+    w.ec = carve_ec(ec, ec_occ);
+    w.eh = carve_ec(eh, eh_occ);
+    w.eh_cand = (uint32_t*)take(eh && eh->n ? 4 * (int64_t)kEhK * eh->n : 0);
     w.hot_nw = (int)((hot_batch + kHotWin - 1) / kHotWin);
     w.hot_hist = nullptr;
     w.hot_cnt = nullptr;
@@ -2565,13 +2703,14 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
 // over the single-chunk columns (k_sgd_exact) — the plan is off the update's critical path.
 inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, const Grouped& out, hipStream_t s,
-                             uint32_t ec_mask) {
+                             uint32_t ec_mask, const EhMap& eh, hipEvent_t cand_ready) {
+    if (eh.mask) ET_HIP_CHECK(hipStreamWaitEvent(s, cand_ready, 0));  // k_eh_pick's candidates
     const int64_t mmax = n / chunk + 2;
     const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
     const int64_t tmax = chain_tiles_max(n, chunk);
     const unsigned tg = (unsigned)(tmax < 8192 ? tmax : 8192);
-    hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask,
-                       out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
+    hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask, eh,
+                       w.eh_cand, out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
                        w.chain_tile_col);
     const bool s1 = chain_fed(false);  // S = 1 plans: entries = occurrences, no run counts
     if (!s1)
@@ -2740,6 +2879,8 @@ inline unsigned env_uint(const char* name, unsigned dflt) {
 struct ChainRun {
     hipStream_t ec_side = nullptr;
     uint32_t ec_ncols = 0;
+    hipStream_t eh_side = nullptr;  // the early hot columns (ET_EH)
+    uint32_t eh_ncols = 0;
     hipStream_t side = nullptr;
 };
 
@@ -2838,9 +2979,18 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         // off — their helper was latency-bound, and the plain items are numbered per
         // quarter (kQuadItems) since the quad walk
         const unsigned hf_wg = 0u;
-        rc = launch_chains<MODE, NT>(pack, ntables, w.ec_counters, w.ec_chains, w.ec_order,
-                                     w.ec_info, w.ec_nocc, w.ec_ent, ns, eta32, eta64, hf_wg, eb,
+        rc = launch_chains<MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
+                                     w.ec.info, w.ec.nocc, w.ec.ent, ns, eta32, eta64, hf_wg, eb,
                                      cr.ec_side, (excl & 1u) != 0, chain_fed(true));
+        if (rc != ET_OK) return rc;
+    }
+    if (cr.eh_side) {
+        static const unsigned eh_wg = env_uint("ET_EH_WG", 32u);
+        const int64_t items = (int64_t)cr.eh_ncols * ns;
+        const unsigned eb = (unsigned)(cdiv64(items, 4) < eh_wg ? cdiv64(items, 4) : eh_wg);
+        rc = launch_chains<MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
+                                     w.eh.info, w.eh.nocc, w.eh.ent, ns, eta32, eta64, 0u, eb,
+                                     cr.eh_side, (excl & 1u) != 0, chain_fed(true));
         if (rc != ET_OK) return rc;
     }
     rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
@@ -3054,25 +3204,37 @@ inline int validate_update(const et_update_desc* descs, int ntables, int64_t* n_
 
 // Early-chain tables of these descriptors (ec_table) and their occurrences; the list
 // sizes the workspace whatever the flags, and et_sparse_sgd uses it in exact Float32 mode.
-inline EcList ec_list(const et_update_desc* descs, int ntables, int64_t* occ) {
+// hot = true: the big tables' hot-column list (eh_table, kEhK slots each; empty unless ET_EH).
+inline EcList ec_list(const et_update_desc* descs, int ntables, int64_t* occ, bool hot = false) {
     EcList ec;
     ec.n = 0;
     ec.mask = 0;
+    ec.hot = hot ? 1 : 0;
     ec.blk0[0] = ec.col0[0] = ec.cb0[0] = 0;
     *occ = 0;
+    if (hot && !eh_enabled()) return ec;
     for (int t = 0; t < ntables; ++t) {
         const et_update_desc& d = descs[t];
-        if (!ec_table(d)) continue;
+        if (hot ? !eh_table(d) : !ec_table(d)) continue;
         const uint32_t nb = (uint32_t)cdiv64(d.batch, kEcBags);
+        const uint32_t cols = hot ? (uint32_t)kEhK : (uint32_t)d.nrows;
         ec.t[ec.n] = t;
         ec.mask |= 1u << t;
         ec.blk0[ec.n + 1] = ec.blk0[ec.n] + nb;
-        ec.col0[ec.n + 1] = ec.col0[ec.n] + (uint32_t)d.nrows;
-        ec.cb0[ec.n + 1] = ec.cb0[ec.n] + nb * (uint32_t)d.nrows;
+        ec.col0[ec.n + 1] = ec.col0[ec.n] + cols;
+        ec.cb0[ec.n + 1] = ec.cb0[ec.n] + nb * cols;
         *occ += d.pool * d.batch;
         ++ec.n;
     }
     return ec;
+}
+
+inline EhMap eh_map(const EcList& eh) {
+    EhMap m;
+    m.mask = eh.hot ? eh.mask : 0u;
+    for (int t = 0; t < ET_MAX_TABLES_PER_LAUNCH; ++t) m.e[t] = 0;
+    for (int e = 0; e < eh.n && eh.hot; ++e) m.e[eh.t[e]] = (int8_t)e;
+    return m;
 }
 
 // Exact Float32 mode: columns of more occurrences than this are serial chains
@@ -3103,9 +3265,11 @@ inline bool ec_enabled() {
 // stream captures every branch.  The fork/join events are shared, so a call that uses
 // the side streams holds `mu` from its first fork to its last join.
 struct SideStreams {
+    static constexpr int kN = 3;  // early chains, regular chains, early hot columns (ET_EH)
     std::mutex mu;
-    hipStream_t st[2] = {nullptr, nullptr};
-    hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+    hipStream_t st[kN] = {nullptr, nullptr, nullptr};
+    hipEvent_t fork[kN] = {nullptr, nullptr, nullptr}, join[kN] = {nullptr, nullptr, nullptr};
+    hipEvent_t cand = nullptr;  // the hot-column candidates are picked (k_eh_pick)
 };
 
 inline SideStreams* side_streams() {
@@ -3115,15 +3279,16 @@ inline SideStreams* side_streams() {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
     SideStreams& ss = streams[dev];
     std::lock_guard<std::mutex> lk(init_mu);
-    if (!ss.st[1]) {
+    if (!ss.cand) {
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < SideStreams::kN; ++i)
             if ((!ss.fork[i] && hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming)) ||
                 (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
                 (!ss.st[i] && hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking,
                                                           greatest)))
                 return nullptr;
+        if (hipEventCreateWithFlags(&ss.cand, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
     return &ss;
 }
@@ -3134,7 +3299,7 @@ struct SideFork {
     SideStreams* ss = nullptr;
     hipStream_t main = nullptr;
     std::unique_lock<std::mutex> lk;
-    bool forked[2] = {false, false};
+    bool forked[SideStreams::kN] = {false, false, false};
     SideFork(SideStreams* s, hipStream_t m) : ss(s), main(m) {
         if (ss) lk = std::unique_lock<std::mutex>(ss->mu);
     }
@@ -3149,7 +3314,7 @@ struct SideFork {
         return ss->st[i];
     }
     ~SideFork() {
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < SideStreams::kN; ++i)
             if (forked[i]) {
                 (void)hipEventRecord(ss->join[i], ss->st[i]);
                 (void)hipStreamWaitEvent(main, ss->join[i], 0);
@@ -3157,19 +3322,31 @@ struct SideFork {
     }
 };
 
-// The early-chain plan (k_ec_count -> k_ec_plan -> k_ec_emit) on stream `s`.
+// The early-chain plan (k_ec_count -> k_ec_plan -> k_ec_emit) on stream `s`; for the
+// hot-column list (ec.hot) after picking the candidates (k_eh_pick), whose completion
+// `cand_ready` records for the regular plan (k_chain_tiles skips the candidates).
 inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chunk,
-                          const UpdateWs& w, int ns, hipStream_t s) {
+                          const UpdateWs::EcWs& w, const uint32_t* cand_c, int ns, hipStream_t s,
+                          hipEvent_t cand_ready = nullptr) {
     const uint32_t M = ec.col0[ec.n];
-    ET_HIP_CHECK(hipMemsetAsync(w.ec_counters, 0, 4 * kCntSlots, s));
-    hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_stats);
+    uint32_t* cand = const_cast<uint32_t*>(cand_c);
+    if (ec.hot) {
+        // ET_EH_MIN: the expected occurrences of a candidate (tests: small batches)
+        static const uint32_t min_occ = env_uint("ET_EH_MIN", kEhMinOcc);
+        hipLaunchKernelGGL(k_eh_pick, dim3(ec.n), dim3(1024), 0, s, pack, ec, min_occ, cand);
+        ET_LAUNCH_CHECK("k_eh_pick");
+        if (cand_ready) ET_HIP_CHECK(hipEventRecord(cand_ready, s));
+    }
+    ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
+    hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.stats,
+                       cand_c);
     hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
-                       w.ec_stats, w.ec_boff, w.ec_cnt, w.ec_nocc, w.ec_info, w.ec_chains,
-                       w.ec_ent, w.ec_counters, chain_fed(true) ? 0 : 4);
-    hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.ec_info, w.ec_nocc, ns,
-                       w.ec_order, w.ec_counters);
-    hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.ec_boff,
-                       w.ec_info, w.ec_ent);
+                       w.stats, w.boff, w.cnt, w.nocc, w.info, w.chains, w.ent, w.counters,
+                       chain_fed(true) ? 0 : 4, cand_c);
+    hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.info, w.nocc, ns, w.order,
+                       w.counters);
+    hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.boff,
+                       w.info, w.ent, cand_c);
     ET_LAUNCH_CHECK("k_ec_emit");
     return ET_OK;
 }
@@ -3192,9 +3369,11 @@ extern "C" int et_sgd_workspace_size(const et_update_desc* descs, int32_t ntable
     int nhot;
     int64_t hb, hbytes;
     et::hot_sizes(descs, ntables, &nhot, &hb, &hbytes);
-    int64_t ec_occ;
+    int64_t ec_occ, eh_occ;
     const et::EcList ec = et::ec_list(descs, ntables, &ec_occ);
-    *bytes = et::carve_update_ws(nullptr, n, pdim, et::kChunk, nhot, hb, hbytes, &ec, ec_occ).bytes;
+    const et::EcList eh = et::ec_list(descs, ntables, &eh_occ, true);
+    *bytes = et::carve_update_ws(nullptr, n, pdim, et::kChunk, nhot, hb, hbytes, &ec, ec_occ, &eh,
+                                 eh_occ).bytes;
     return ET_OK;
 }
 
@@ -3257,10 +3436,11 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     int64_t hb, hbytes;
     uint64_t soff[ET_MAX_TABLES_PER_LAUNCH];
     et::hot_sizes(descs, ntables, &nhot, &hb, &hbytes, soff);
-    int64_t ec_occ;
+    int64_t ec_occ, eh_occ;
     const et::EcList ec = et::ec_list(descs, ntables, &ec_occ);
+    const et::EcList eh = et::ec_list(descs, ntables, &eh_occ, true);
     et::UpdateWs w = et::carve_update_ws(static_cast<char*>(workspace), n, pdim, et::kChunk,
-                                         nhot, hb, hbytes, &ec, ec_occ);
+                                         nhot, hb, hbytes, &ec, ec_occ, &eh, eh_occ);
     if (!workspace || ws_bytes < w.bytes)
         return et::fail(ET_ERR_WORKSPACE, "workspace of %lld bytes needed",
                         (long long)w.bytes);
@@ -3316,6 +3496,8 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     // planned from the index arrays at the start of the index phase) from the start of the
     // call, the regular ones once the index phase has planned them
     const bool use_ec = chain && ec.n > 0 && et::ec_enabled();
+    const bool use_eh = chain && eh.n > 0 && et::ec_enabled();  // eh.n > 0 only under ET_EH
+    const et::EhMap ehm = et::eh_map(use_eh ? eh : et::EcList{});
     et::SideStreams* sides = chain ? et::side_streams() : nullptr;
     if (chain && !sides) return et::fail(ET_ERR_HIP, "sparse SGD: side streams unavailable");
     et::SideFork fork(sides, s);
@@ -3324,7 +3506,17 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
         ec_side = fork.fork(0);
         if (!ec_side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
         if (!apply_only) {
-            rc = et::launch_ec_plan(pack, ec, chunk, w, (pdim + 63) / 64, ec_side);
+            rc = et::launch_ec_plan(pack, ec, chunk, w.ec, nullptr, (pdim + 63) / 64, ec_side);
+            if (rc != ET_OK) return rc;
+        }
+    }
+    hipStream_t eh_side = nullptr;
+    if (use_eh) {
+        eh_side = fork.fork(2);
+        if (!eh_side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
+        if (!apply_only) {
+            rc = et::launch_ec_plan(pack, eh, chunk, w.eh, w.eh_cand, (pdim + 63) / 64, eh_side,
+                                    sides->cand);
             if (rc != ET_OK) return rc;
         }
     }
@@ -3340,6 +3532,8 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     if (chain) {
         cr.ec_side = ec_side;
         cr.ec_ncols = use_ec ? ec.col0[ec.n] : 0u;
+        cr.eh_side = eh_side;
+        cr.eh_ncols = use_eh ? eh.col0[eh.n] : 0u;
         // the regular chains' plan: on their side stream beside the chunk pass (default), or
         // on the caller's stream before it (ET_PLAN_SIDE=0: the chains start earlier, the
         // chunk pass later)
@@ -3349,14 +3543,14 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
         }();
         if (!apply_only && !plan_side) {
             rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, s,
-                                       use_ec ? ec.mask : 0u);
+                                       use_ec ? ec.mask : 0u, ehm, sides->cand);
             if (rc != ET_OK) return rc;
         }
         cr.side = fork.fork(1);  // after the index phase's chunk records (and the plan)
         if (!cr.side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
         if (!apply_only && plan_side) {
             rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, cr.side,
-                                       use_ec ? ec.mask : 0u);
+                                       use_ec ? ec.mask : 0u, ehm, sides->cand);
             if (rc != ET_OK) return rc;
         }
     }

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round 4: early hot columns of the big tables (ET_EH) and fed chains (asm gatherer):
+# parity under each knob, config-4 exact timings, timelines.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/eh; mkdir -p $OUT
+T="tests/test_gpu_early_chains.py tests/test_gpu_update.py"
+ET_EH=1 ET_EH_MIN=300 timeout -k 10 300 python3 -u -m pytest $T -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_eh.log 2>&1 || { echo EH_TEST_FAIL; tail -30 $OUT/pytest_eh.log; exit 1; }
+echo "eh $(tail -1 $OUT/pytest_eh.log)"
+for r in 1 2; do for v in "ET_EH=0" "ET_EH=1" "ET_EH=1 ET_PLAN_SIDE=0"; do
+  env $v timeout -k 10 200 python3 tools/exact_cfg4.py exact > $OUT/cfg4.txt 2>&1 || { echo CFG4_FAIL $v; tail -5 $OUT/cfg4.txt; exit 1; }
+  echo "$v $(tail -1 $OUT/cfg4.txt)"
+done; done
+ET_EH=1 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_fullsize.py -x -q -m gpu -k exact --timeout 300 --timeout-method thread > $OUT/pytest_eh_full.log 2>&1 || { echo EH_FULL_FAIL; tail -30 $OUT/pytest_eh_full.log; exit 1; }
+echo "eh full $(tail -1 $OUT/pytest_eh_full.log)"
+ET_EH=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv \
+  -- python3 tools/exact_cfg4.py exact > $OUT/exact_traced.txt 2>&1 || { echo TRACE_FAIL; tail -5 $OUT/exact_traced.txt; exit 1; }
+f=$(ls $OUT/prof/*/run_kernel_trace.csv $OUT/prof/run_kernel_trace.csv 2>/dev/null | head -1)
+python3 tools/upd_timeline.py "$f" > $OUT/exact_timeline.txt && echo "timeline eh" && grep -E "chains|sgd_exact|eh_pick|ec_emit|total" $OUT/exact_timeline.txt
+ET_CHAIN_FED=2 timeout -k 10 300 python3 -u -m pytest $T -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_fed.log 2>&1 || { echo FED_TEST_FAIL; tail -30 $OUT/pytest_fed.log; exit 1; }
+echo "fed $(tail -1 $OUT/pytest_fed.log)"
+for v in "ET_CHAIN_FED=1" "ET_CHAIN_FED=2" "ET_CHAIN_FED=1 ET_EH=1"; do
+  env $v timeout -k 10 200 python3 tools/exact_cfg4.py exact > $OUT/cfg4.txt 2>&1 || { echo CFG4_FAIL $v; tail -5 $OUT/cfg4.txt; exit 1; }
+  echo "$v $(tail -1 $OUT/cfg4.txt)"
+done

@@ -18,10 +18,14 @@ for q in range(i, j):
     if "k_pooled" in n or "k_fill" in n or "elementwise" in n.lower() or "copy" in n.lower():
         break
     end = q
-t0 = prev = int(rows[i]["Start_Timestamp"])
+# the early-chain plans (side streams) may start just before k_build_keys
+while i > 0 and ("k_ec_" in rows[i - 1]["Kernel_Name"] or "k_eh_" in rows[i - 1]["Kernel_Name"]):
+    i -= 1
+t0 = prev = last = int(rows[i]["Start_Timestamp"])
 for r in rows[i:end + 1]:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     print(f"{(s - t0) / 1e3:8.1f} gap={(s - prev) / 1e3:6.1f} dur={(e - s) / 1e3:8.1f} "
           f"{r['Kernel_Name'][:60]}")
     prev = e
-print(f"total {(prev - t0) / 1e3:.1f} us")
+    last = max(last, e)
+print(f"total {(last - t0) / 1e3:.1f} us")
