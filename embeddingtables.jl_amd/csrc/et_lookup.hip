@@ -24,6 +24,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <utility>
+#include <vector>
+
 namespace et {
 
 struct LookupPack {
@@ -499,9 +503,8 @@ template <typename T, typename A, int D, int U, bool NT, bool NTI, bool SG = fal
 __device__ __forceinline__ void striped_body(const LookupPack& pack, const StripeMap& sm,
                                              int ntables, int64_t batch, T* __restrict__ dst,
                                              int64_t ld_dst, int rounds, int64_t stripe_chunks,
-                                             int64_t nchunks) {
-    const int x = blockIdx.x % kXcds;
-    const int64_t slot = blockIdx.x / kXcds;
+                                             int64_t nchunks, int x = blockIdx.x % kXcds,
+                                             int64_t slot = blockIdx.x / kXcds) {
     const int k = (int)(slot % ntables);
     const int64_t j = slot / ntables;
     const uint32_t e = sm.entry[x][k];
@@ -561,6 +564,81 @@ __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, Str
         g_tl[blockIdx.x][1] = make_uint4(t, xcc, hw, gridDim.x);
     }
 #endif
+}
+
+// Per-XCD work queues (ET_SCHED=queue): the same stripe map, but a
+// workgroup takes its item from the queue of the XCD it actually runs on (one atomic head
+// per XCD, items in the static schedule's order) and, once that queue is empty, from the
+// other XCDs' queues, so an XCD whose stripes run faster (the static schedule's XCDs
+// finished between 1184 and 1266 us, profiles/r03/b/wg_timeline.json) takes over the
+// tail of the slower ones.  The grid has exactly as many workgroups as items, so every
+// workgroup finds one; the last workgroup to finish resets the heads (atomically) for the
+// next launch on the same stream.  Each stream has a queue block of its own (kQueueSlots
+// per device; launches on one stream never overlap) and a captured launch keeps the static
+// schedule, so a graph replayed on another stream cannot share a block.  Which workgroup
+// sums which bags never changes a result: bit-identical to the static schedule.
+constexpr int kQueueSlots = 64;
+struct XcdQueue {
+    uint32_t head[kXcds];
+    uint32_t done;
+    uint32_t pad[32 - kXcds - 1];  // one 128-byte line per block
+};
+__device__ XcdQueue g_xcd_queue[kQueueSlots];
+
+template <typename T, typename A, int D, int U, bool NT, bool SG>
+__global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, StripeMap sm,
+                                                           int ntables, int64_t batch,
+                                                           T* __restrict__ dst, int64_t ld_dst,
+                                                           int rounds, int64_t stripe_chunks,
+                                                           int64_t nchunks, int qslot) {
+    __shared__ uint32_t s_item;
+    XcdQueue& q = g_xcd_queue[qslot];
+    const uint32_t per = (uint32_t)(ntables * stripe_chunks);  // items per XCD
+    if (threadIdx.x == 0) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        uint32_t it = ~0u;
+        for (uint32_t k = 0; k < (uint32_t)kXcds; ++k) {
+            const uint32_t x = (xcc + k) & (uint32_t)(kXcds - 1);
+            const uint32_t h = atomicAdd(&q.head[x], 1u);
+            if (h < per) {
+                it = x * per + h;
+                break;
+            }
+        }
+        s_item = it;
+    }
+    __syncthreads();
+    const uint32_t it = s_item;
+    if (it != ~0u)
+        striped_body<T, A, D, U, NT, false, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
+                                                stripe_chunks, nchunks, (int)(it / per),
+                                                (int64_t)(it % per));
+    if (threadIdx.x == 0 && atomicAdd(&q.done, 1u) == gridDim.x - 1u) {  // the last one
+        for (int x = 0; x < kXcds; ++x) atomicExch(&q.head[x], 0u);
+        atomicExch(&q.done, 0u);
+    }
+}
+
+// The queue block of stream s on the current device, or -1 (capturing, or more than
+// kQueueSlots streams have launched queued lookups on this device).
+inline int xcd_queue_slot(hipStream_t s) {
+    static std::mutex mu;
+    static std::vector<std::pair<int, hipStream_t>> owners;  // slot -> (device, stream)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return -1;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    std::lock_guard<std::mutex> lk(mu);
+    int mine = 0;
+    for (const auto& o : owners) {
+        if (o.first != dev) continue;
+        if (o.second == s) return mine;
+        ++mine;
+    }
+    if (mine >= kQueueSlots) return -1;
+    owners.emplace_back(dev, s);
+    return mine;
 }
 
 // The same kernel held to 64 VGPRs (8 waves per SIMD instead of 7): ET_W8=1 experiment.
@@ -713,6 +791,7 @@ inline int rounds_for(int64_t batch, int64_t bags_per_round, int ntables) {
 // Scheduling knobs (read once; for experiments — the defaults are the tuned choice).
 struct LookupTuning {
     int striped = 1;               // ET_SCHED=linear disables the XCD stripe schedule
+    int queued = 0;                // ET_SCHED=queue: per-XCD work queues (k_pooled_vec_queued)
     // Tables larger than the 256 MiB Infinity Cache cannot stay cache resident: their
     // rows are loaded non-temporally so they do not evict the light tables from L2
     // (measured -5% on the Criteo mix; nt on the cache-resident mid-size tables hurts).
@@ -731,7 +810,10 @@ struct LookupTuning {
 inline const LookupTuning& tuning() {
     static LookupTuning t = [] {
         LookupTuning v;
-        if (const char* e = getenv("ET_SCHED")) v.striped = strcmp(e, "linear") != 0;
+        if (const char* e = getenv("ET_SCHED")) {
+            v.striped = strcmp(e, "linear") != 0;
+            v.queued = strcmp(e, "queue") == 0;
+        }
         if (const char* e = getenv("ET_NTLOAD")) v.ntload = atoi(e);
         if (const char* e = getenv("ET_NTLOAD_BYTES")) v.ntload_bytes = atoll(e);
         if (const char* e = getenv("ET_NTIDX")) v.ntidx = atoi(e);
@@ -827,6 +909,24 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
         const int64_t grid = (int64_t)kXcds * n * stripe_chunks;
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+        const int qslot = tuning().queued ? xcd_queue_slot(s) : -1;
+        if (qslot >= 0 && grid < 0xffffffffll) {
+            if constexpr (kSG) {
+                if (sg) {
+                    hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, true>),
+                                       dim3((unsigned)grid), dim3(256), 0, s, pack, sm, n, batch,
+                                       reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
+                                       nchunks, qslot);
+                    ET_LAUNCH_CHECK("k_pooled_vec_queued");
+                    return ET_OK;
+                }
+            }
+            hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, false>), dim3((unsigned)grid),
+                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               ld_dst, rounds, stripe_chunks, nchunks, qslot);
+            ET_LAUNCH_CHECK("k_pooled_vec_queued");
+            return ET_OK;
+        }
         if constexpr (kSG) {
             if (sg && tuning().w8) {
                 hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT, false, true>),

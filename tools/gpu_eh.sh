@@ -23,3 +23,10 @@ for v in "ET_CHAIN_FED=1" "ET_CHAIN_FED=2" "ET_CHAIN_FED=1 ET_EH=1"; do
   env $v timeout -k 10 200 python3 tools/exact_cfg4.py exact > $OUT/cfg4.txt 2>&1 || { echo CFG4_FAIL $v; tail -5 $OUT/cfg4.txt; exit 1; }
   echo "$v $(tail -1 $OUT/cfg4.txt)"
 done
+# per-XCD work queues for the headline lookup (ET_SCHED=queue): parity, then A/B twice
+ET_SCHED=queue timeout -k 10 400 python3 -u -m pytest tests/test_gpu_fullsize.py -x -q -m gpu -k config3 --timeout 300 --timeout-method thread > $OUT/pytest_queue.log 2>&1 || { echo QUEUE_TEST_FAIL; tail -30 $OUT/pytest_queue.log; exit 1; }
+echo "queue $(tail -1 $OUT/pytest_queue.log)"
+for r in 1 2; do for v in "ET_SCHED=stripe" "ET_SCHED=queue"; do
+  env $v timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-extra --cpu-seconds 2 > $OUT/bench_q.txt 2>&1 || { echo BENCH_FAIL $v; tail -5 $OUT/bench_q.txt; exit 1; }
+  echo "$v $(tail -1 $OUT/bench_q.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["roofline"]["frac"], d["roofline"].get("achieved"))')"
+done; done
