@@ -1235,7 +1235,7 @@ __device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32
 // The early hot-column candidates of the big tables (ET_EH, see EcList below): kEhK
 // ascending columns per table, ~0 past the last; EhMap says which tables have a list and
 // where it is.
-constexpr int kEhK = 64;  // candidate columns per table
+constexpr int kEhK = 16;  // candidate columns per table
 struct EhMap {
     uint32_t mask;                      // bit t: table t has a candidate list
     int8_t e[ET_MAX_TABLES_PER_LAUNCH];  // its entry: the list at cand + e * kEhK
@@ -1266,7 +1266,13 @@ __global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntabl
                                                       uint32_t sent, uint32_t* __restrict__ tile0,
                                                       uint32_t* __restrict__ tile_col) {
     __shared__ uint32_t lds16[16];
+    __shared__ uint32_t sc[ET_MAX_TABLES_PER_LAUNCH * kEhK];  // the candidate lists
     const uint32_t M = counters[kCntM];
+    if (eh.mask) {
+        const int ne = __popc(eh.mask);
+        for (int i = threadIdx.x; i < ne * kEhK; i += 1024) sc[i] = cand[i];
+        __syncthreads();
+    }
     uint32_t carry = 0;
     for (uint32_t b0 = 0; b0 < M; b0 += 1024) {
         const uint32_t m = b0 + threadIdx.x;
@@ -1277,7 +1283,7 @@ __global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntabl
             const int t = k0 == sent ? 0 : table_of_key(pack, ntables, k0);
             const bool early = k0 == sent || ((ec_mask >> t) & 1u) ||
                                (((eh.mask >> t) & 1u) &&
-                                eh_slot(cand + eh.e[t] * kEhK, k0 - pack.row_off[t]) >= 0);
+                                eh_slot(sc + eh.e[t] * kEhK, k0 - pack.row_off[t]) >= 0);
             v = early ? 0u : cdiv_u32(se - ss, kChainTile);
         }
         uint32_t total;
@@ -1608,8 +1614,8 @@ constexpr uint32_t kHfMinOcc = 65536;  // helper-fed chains: at least this many 
 // same k_ec_* kernels (a bag's indices are matched against the table's candidate list); a
 // candidate with more than `chunk` occurrences is a chain there, and the regular plan skips
 // it (k_chain_tiles), so every column is summed exactly once.
-constexpr int kEhSampleBags = 4096;     // bags sampled by k_eh_pick
-constexpr uint32_t kEhMinOcc = 4096;    // expected occurrences of a candidate
+constexpr int kEhSampleBags = 1024;     // bags sampled by k_eh_pick
+constexpr uint32_t kEhMinOcc = 32768;   // expected occurrences of a candidate (ET_EH_MIN)
 constexpr int kEhHash = 4096;           // LDS hash slots of the sample count
 constexpr int kEhProbes = 16;           // linear probes per occurrence
 
@@ -1662,7 +1668,9 @@ __global__ __launch_bounds__(1024) void k_eh_pick(UpdatePack pack, EcList ec, ui
         if (c >= (uint64_t)d.nrows) continue;
         uint32_t h = ((uint32_t)c * 2654435761u) >> 20;  // 12 bits
         for (int probe = 0; probe < kEhProbes; ++probe, h = (h + 1) & (kEhHash - 1)) {
-            const uint32_t prev = atomicCAS(&hk[h], ~0u, (uint32_t)c);
+            // the hot columns' slots are taken early: a plain read finds them without a CAS
+            const uint32_t seen = hk[h];
+            const uint32_t prev = seen == (uint32_t)c ? seen : atomicCAS(&hk[h], ~0u, (uint32_t)c);
             if (prev == ~0u || prev == (uint32_t)c) {
                 atomicAdd(&hc[h], 1u);
                 break;
