@@ -714,7 +714,7 @@ def main():
         "samples_per_s": B * args.steps / elapsed,
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_pooled_vec_striped<float,float,128,8,NT,0,SG=1> (scalar-addressed)",
+            "kernel": "k_pooled_vec_queued<float,float,128,8,NT,SG=1> (scalar-addressed, per-XCD queues)",
             # achieved = HBM-compulsory bytes (rows of the tables larger than the 256 MiB
             # Infinity Cache + all indices + the output) / average launch time: a lower
             # bound on the DRAM rate, so frac <= 1; the cache-inclusive SURVEY.md §8d

@@ -791,7 +791,10 @@ inline int rounds_for(int64_t batch, int64_t bags_per_round, int ntables) {
 // Scheduling knobs (read once; for experiments — the defaults are the tuned choice).
 struct LookupTuning {
     int striped = 1;               // ET_SCHED=linear disables the XCD stripe schedule
-    int queued = 0;                // ET_SCHED=queue: per-XCD work queues (k_pooled_vec_queued)
+    // per-XCD work queues (k_pooled_vec_queued) by default: headline 1.261-1.262 vs
+    // 1.270-1.271 ms for the static stripe schedule (A/B twice on one box, round 4,
+    // profiles/r04/queue_ab.txt); ET_SCHED=stripe restores the static schedule
+    int queued = 1;
     // Tables larger than the 256 MiB Infinity Cache cannot stay cache resident: their
     // rows are loaded non-temporally so they do not evict the light tables from L2
     // (measured -5% on the Criteo mix; nt on the cache-resident mid-size tables hurts).
@@ -812,7 +815,7 @@ inline const LookupTuning& tuning() {
         LookupTuning v;
         if (const char* e = getenv("ET_SCHED")) {
             v.striped = strcmp(e, "linear") != 0;
-            v.queued = strcmp(e, "queue") == 0;
+            v.queued = v.striped && strcmp(e, "stripe") != 0;
         }
         if (const char* e = getenv("ET_NTLOAD")) v.ntload = atoi(e);
         if (const char* e = getenv("ET_NTLOAD_BYTES")) v.ntload_bytes = atoll(e);

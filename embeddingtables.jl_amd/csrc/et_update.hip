@@ -1639,10 +1639,12 @@ inline bool eh_table(const et_update_desc& d) {
            d.pool <= kEcMaxPool && d.batch > 0 && d.batch <= kEcMaxBatch && d.dim > 0;
 }
 
+// On by default: config-4 exact update 4.05-4.06 ms with, 4.24-4.25 without (the exact
+// grid cap on, A/B twice on one box, profiles/r04/ab_exact_grid.txt); ET_EH=0 turns it off.
 inline bool eh_enabled() {
     static const bool v = [] {
         const char* e = getenv("ET_EH");
-        return e ? atoi(e) != 0 : false;
+        return e ? atoi(e) != 0 : true;
     }();
     return v;
 }
@@ -2055,8 +2057,11 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
         const uint32_t* e = reinterpret_cast<const uint32_t*>(
             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)eb) |
             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(eb >> 32)) << 32);
+        // how & 8: timing experiment only (ET_CHAIN_FAKE=1, wrong results): every entry
+        // loads gradient row 0 (cache-resident), so the walk runs without HBM latency
         const float acc = chain_walk_quad(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
-                                          (uint32_t)d.batch * ld * 4u, 4u * fc, 4u * ld);
+                                          (uint32_t)d.batch * ld * 4u, 4u * fc,
+                                          how & 8 ? 0u : 4u * ld);
         if (lane < 16 && f < d.dim) {
             float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
             store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
@@ -2085,17 +2090,18 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
     } else {
         // range batch * ld * 4 bytes: a padding entry (bag = batch) loads +0
         const i32x4 rs = chain_rsrc(delta, (uint32_t)d.batch * ld * 4u);
+        const uint32_t ld4 = how & 8 ? 0u : 4u * ld;  // ET_CHAIN_FAKE (timing only)
         switch (c.S) {
-            case 1: acc = chain_walk_asm<1>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
-            case 2: acc = chain_walk_asm<2>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
-            case 4: acc = chain_walk_asm<4>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+            case 1: acc = chain_walk_asm<1>(e, c.ngr, rs, 4u * fc, ld4, 0.0f); break;
+            case 2: acc = chain_walk_asm<2>(e, c.ngr, rs, 4u * fc, ld4, 0.0f); break;
+            case 4: acc = chain_walk_asm<4>(e, c.ngr, rs, 4u * fc, ld4, 0.0f); break;
             case 8:
-                acc = how & 4 ? chain_walk_ring<8>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f)
-                              : chain_walk_asm<8>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f);
+                acc = how & 4 ? chain_walk_ring<8>(e, c.ngr, rs, 4u * fc, ld4, 0.0f)
+                              : chain_walk_asm<8>(e, c.ngr, rs, 4u * fc, ld4, 0.0f);
                 break;
             default:
-                acc = how & 4 ? chain_walk_ring<16>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f)
-                              : chain_walk_asm<16>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f);
+                acc = how & 4 ? chain_walk_ring<16>(e, c.ngr, rs, 4u * fc, ld4, 0.0f)
+                              : chain_walk_asm<16>(e, c.ngr, rs, 4u * fc, ld4, 0.0f);
                 break;
         }
     }
@@ -2897,16 +2903,18 @@ template <int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
                   const uint32_t* order, const uint2* info, const uint32_t* nocc,
                   const uint32_t* ent, int ns, float eta32, double eta64, unsigned nhf,
-                  unsigned nb, hipStream_t s, bool excl = false, bool fed = false) {
+                  unsigned nb, hipStream_t s, bool excl = false, bool fed = false,
+                  uint32_t lds_req = 0u) {
     static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++;
         // experiments: ET_CHAIN_QUAD=0 walks S = 1 chains with the 64-feature asm loop
         const char* e = getenv("ET_CHAIN_ASM");
         const char* q = getenv("ET_CHAIN_QUAD");
         const char* m = getenv("ET_QUAD_MIN");  // experiments: quad-walk threshold
         const char* r = getenv("ET_CHAIN_RING");  // S >= 8: the 64-deep ring loop
+        const char* f = getenv("ET_CHAIN_FAKE");  // timing only: every load from row 0
         const int qmin = m ? atoi(m) : kQuadMinGroups;
         return (e && atoi(e) == 0 ? 1 : 0) | (q && atoi(q) == 0 ? 2 : 0) |
-               (r && atoi(r) != 0 ? 4 : 0) | (qmin << 4);
+               (r && atoi(r) != 0 ? 4 : 0) | (f && atoi(f) != 0 ? 8 : 0) | (qmin << 4);
     }();
     // experiments: ET_CHAIN_LDS = KiB reserved per chain workgroup (160: a whole CU)
     static const uint32_t lds = [] {
@@ -2941,14 +2949,15 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         ET_LAUNCH_CHECK("k_sgd_chains_fed");
         return ET_OK;
     }
+    const uint32_t lds_use = lds_req != 0u && lds_req <= lds ? lds_req : lds;
     if (excl && nhf == 0) {
-        hipLaunchKernelGGL((k_sgd_chains_x<MODE, NT>), dim3(nb), dim3(256), lds, s, pack,
+        hipLaunchKernelGGL((k_sgd_chains_x<MODE, NT>), dim3(nb), dim3(256), lds_use, s, pack,
                            ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64,
                            plain, 0u);
         ET_LAUNCH_CHECK("k_sgd_chains_x");
         return ET_OK;
     }
-    hipLaunchKernelGGL((k_sgd_chains<MODE, NT>), dim3(nhf + nb), dim3(256), lds, s, pack,
+    hipLaunchKernelGGL((k_sgd_chains<MODE, NT>), dim3(nhf + nb), dim3(256), lds_use, s, pack,
                        ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64, plain,
                        nhf);
     ET_LAUNCH_CHECK("k_sgd_chains");
@@ -2965,6 +2974,14 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                      const VecGroups& vg, bool any_generic, hipStream_t s, unsigned grid,
                      ChainRun cr) {
     const int ns = (pdim + 63) / 64;
+    // The chunk pass + singles of the exact mode run at most 512 + 512 grid-stride
+    // workgroups: fewer in flight than the split mode's 16384 + 16384 leaves the fabric to
+    // the latency-bound chains beside it (config 4, A/B twice on one box: 4.22-4.24 ms at
+    // the split mode's grid, 4.05-4.06 at 384-768, 4.20 at 256; the split mode itself is
+    // faster at its own grid, 3.00 vs 3.61 ms; profiles/r04/ab_exact_grid.txt).
+    // ET_EXACT_GRID overrides (experiments).
+    static const unsigned xcap = env_uint("ET_EXACT_GRID", 512u);
+    grid = grid < xcap ? grid : xcap;
     // chain workgroups (one CU each): 32 early, 128 regular, so the regular chains find
     // free CUs when the index phase releases them instead of waiting for early-chain
     // workgroups (config 4, one box, twice: 256/256 4.62-4.63 ms, 32/128 4.19-4.27,
@@ -2975,9 +2992,10 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     // The early chains only (config 4, A/B twice on one box: none 4.02-4.11 ms, early
     // 4.015-4.017, regular 4.33-4.34, both 4.35; profiles/r03/e/ab_chain_excl.txt): the
     // regular chains run beside the chunk pass, which needs those SIMDs more.
+    // Bit 2: the early hot columns (ET_EH) too.
     static const unsigned excl = [] {
         const char* e = getenv("ET_CHAIN_EXCL");
-        return e ? (unsigned)atoi(e) & 3u : 1u;
+        return e ? (unsigned)atoi(e) & 7u : 5u;
     }();
     int rc;
     if (cr.ec_side) {
@@ -2994,11 +3012,15 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
     }
     if (cr.eh_side) {
         static const unsigned eh_wg = env_uint("ET_EH_WG", 32u);
+        // ET_EH_LDS: KiB reserved per hot-column workgroup (experiments; default the chain
+        // launches' one-workgroup-per-CU reservation)
+        static const unsigned eh_lds = env_uint("ET_EH_LDS", 0u) * 1024u;
         const int64_t items = (int64_t)cr.eh_ncols * ns;
         const unsigned eb = (unsigned)(cdiv64(items, 4) < eh_wg ? cdiv64(items, 4) : eh_wg);
         rc = launch_chains<MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
                                      w.eh.info, w.eh.nocc, w.eh.ent, ns, eta32, eta64, 0u, eb,
-                                     cr.eh_side, (excl & 1u) != 0, chain_fed(true));
+                                     cr.eh_side, (excl & 4u) != 0, chain_fed(true),
+                                     eh_lds <= 160u * 1024u ? eh_lds : 0u);
         if (rc != ET_OK) return rc;
     }
     rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
