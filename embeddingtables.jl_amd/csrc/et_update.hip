@@ -1111,6 +1111,13 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
 // cost so the longest chains are dispatched first), k_chain_emit (the entries).  Update phase: the chain role of
 // k_sgd_exact, beside the chunk pass (single-chunk columns) and the singles in ONE
 // launch, so the hottest chains (834,828 adds on the config-4 batch) overlap the rest.
+// A positive integer from the environment (experiment knobs), else dflt.
+inline unsigned env_uint(const char* name, unsigned dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? (unsigned)v : dflt;
+}
+
 constexpr int kChainGroup = kChainAsmTrip;  // entries per trip of the asm loop
 constexpr int kChainPad = kChainAsmPad;     // readable entries past the last trip
 // Issue slots of one entry of a chain at S adds per entry, doubled (et_chain_asm.h:
@@ -1378,8 +1385,10 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             E[k] = wave_sum_u32(E[k]);
-            const uint64_t c = (uint64_t)E[k] * chain_entry_cost2(1u << k);
-            if (k <= kmax && c < bc) bc = c, best = k;  // kmax 0: every entry one occurrence
+            // kmax >> 8: a per-entry latency term (doubled slots, ET_LAT_REG) that favours
+            // fewer, longer entries for latency-bound chains; kmax & 255 the largest log2 S
+            const uint64_t c = (uint64_t)E[k] * (chain_entry_cost2(1u << k) + ((uint32_t)kmax >> 8));
+            if (k <= (kmax & 255) && c < bc) bc = c, best = k;  // 0: every entry one occurrence
         }
         if (lane == 0) {
             cnt[m] = cdiv_u32(E[best], kChainGroup) * kChainGroup + kChainPad;
@@ -1838,8 +1847,8 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
     uint64_t bc = ~0ull;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        const uint64_t cc = (uint64_t)v[1 + k] * chain_entry_cost2(1u << k);
-        if (k <= kmax && cc < bc) bc = cc, best = k;
+        const uint64_t cc = (uint64_t)v[1 + k] * (chain_entry_cost2(1u << k) + ((uint32_t)kmax >> 8));
+        if (k <= (kmax & 255) && cc < bc) bc = cc, best = k;  // as k_chain_choose
     }
     const bool is_chain = v[0] > chunk;  // wave-uniform
     const uint32_t S = is_chain ? (1u << best) : 0u, E = is_chain ? v[1 + best] : 0u;
@@ -2122,16 +2131,17 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
 // (memory bound) take the leftover issue slots.
 constexpr uint32_t kChainReserveLds = 84 * 1024;  // > 80 KiB: one chain workgroup per CU
 
-// ET_CHAIN_FED: chains planned at S = 1 and walked by k_sgd_chains_fed (below) — 1: the
-// early chains, 2: the early and the regular chains.
-inline int chain_fed_level() {
+// ET_CHAIN_FED: chains planned at S = 1 and walked by k_sgd_chains_fed (below), a bit mask
+// of chain lists — 1: the early chains, 2: the regular chains, 4: the early hot columns.
+enum { kFedEarly = 1, kFedRegular = 2, kFedHot = 4 };
+inline int chain_fed_mask() {
     static const int v = [] {
         const char* e = getenv("ET_CHAIN_FED");
         return e ? atoi(e) : 0;
     }();
     return v;
 }
-inline bool chain_fed(bool early) { return chain_fed_level() >= (early ? 1 : 2); }
+inline bool chain_fed(int list) { return (chain_fed_mask() & list) != 0; }
 
 // Helper-fed chains ("HF": the longest early chains, whose runs are long — S >= 8 — and
 // whose columns have at least kHfMinOcc occurrences).  The plain loop spends, per entry of
@@ -2726,14 +2736,16 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask, eh,
                        w.eh_cand, out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
                        w.chain_tile_col);
-    const bool s1 = chain_fed(false);  // S = 1 plans: entries = occurrences, no run counts
+    const bool s1 = chain_fed(kFedRegular);  // S = 1 plans: entries = occurrences, no run counts
     if (!s1)
         hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                            out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
                            w.chain_tile_col, w.chain_tcnt);
+    static const unsigned lat_reg = env_uint("ET_LAT_REG", 0u);
     hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
                        w.mlist, w.counters, w.chain_tile0, s1 ? nullptr : w.chain_tcnt,
-                       w.chain_cnt, w.chain_info, w.chains, s1 ? 0 : 4);
+                       w.chain_cnt, w.chain_info, w.chains,
+                       s1 ? 0 : 4 | (int)lat_reg << 8);
     hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
                        w.chain_info, w.chain_e0, w.chain_order);
     if (s1)
@@ -2881,11 +2893,6 @@ inline bool sgd_chunks_occ5() {
     return v;
 }
 
-inline unsigned env_uint(const char* name, unsigned dflt) {
-    const char* e = getenv(name);
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? (unsigned)v : dflt;
-}
 
 // The chains of an exact update phase: the side stream of the early chains (null: none)
 // and their column count, the side stream of the regular chains (forked from the caller's
@@ -3007,7 +3014,7 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         const unsigned hf_wg = 0u;
         rc = launch_chains<MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
                                      w.ec.info, w.ec.nocc, w.ec.ent, ns, eta32, eta64, hf_wg, eb,
-                                     cr.ec_side, (excl & 1u) != 0, chain_fed(true));
+                                     cr.ec_side, (excl & 1u) != 0, chain_fed(kFedEarly));
         if (rc != ET_OK) return rc;
     }
     if (cr.eh_side) {
@@ -3019,13 +3026,13 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         const unsigned eb = (unsigned)(cdiv64(items, 4) < eh_wg ? cdiv64(items, 4) : eh_wg);
         rc = launch_chains<MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
                                      w.eh.info, w.eh.nocc, w.eh.ent, ns, eta32, eta64, 0u, eb,
-                                     cr.eh_side, (excl & 4u) != 0, chain_fed(true),
+                                     cr.eh_side, (excl & 4u) != 0, chain_fed(kFedHot),
                                      eh_lds <= 160u * 1024u ? eh_lds : 0u);
         if (rc != ET_OK) return rc;
     }
     rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
                                  w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u, reg_wg,
-                                 cr.side, (excl & 2u) != 0, chain_fed(false));
+                                 cr.side, (excl & 2u) != 0, chain_fed(kFedRegular));
     if (rc != ET_OK) return rc;
 #define ET_SGD_EXACT(DD)                                                                       \
     case DD:                                                                                   \
@@ -3370,9 +3377,12 @@ inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chu
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
     hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.stats,
                        cand_c);
+    static const unsigned lat_eh = env_uint("ET_LAT_EH", 0u), lat_ec = env_uint("ET_LAT_EC", 0u);
     hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
                        w.stats, w.boff, w.cnt, w.nocc, w.info, w.chains, w.ent, w.counters,
-                       chain_fed(true) ? 0 : 4, cand_c);
+                       chain_fed(ec.hot ? kFedHot : kFedEarly) ? 0
+                                       : 4 | (int)(ec.hot ? lat_eh : lat_ec) << 8,
+                       cand_c);
     hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.info, w.nocc, ns, w.order,
                        w.counters);
     hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.boff,
