@@ -3309,6 +3309,30 @@ struct SideStreams {
     hipEvent_t cand = nullptr;  // the hot-column candidates are picked (k_eh_pick)
 };
 
+// The side streams' priority: the device's greatest (default), or ET_SIDE_PRIO=0 the
+// least (experiments).
+inline int side_prio(int least, int greatest) {
+    const char* e = getenv("ET_SIDE_PRIO");
+    return e && atoi(e) == 0 ? least : greatest;
+}
+
+// ET_SIDE_CUMASK=1 (experiments): the side streams with a full CU mask, which gives each a
+// hardware queue of its own.
+inline hipError_t side_stream_create(hipStream_t* st, int least, int greatest) {
+    const char* e = getenv("ET_SIDE_CUMASK");
+    if (e && atoi(e) != 0) {
+        int dev = 0, ncu = 0;
+        hipError_t r = hipGetDevice(&dev);
+        if (r == hipSuccess) r = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (r != hipSuccess) return r;
+        uint32_t mask[16];
+        const int words = (ncu + 31) / 32 < 16 ? (ncu + 31) / 32 : 16;
+        for (int k = 0; k < words; ++k) mask[k] = 0xffffffffu;
+        return hipExtStreamCreateWithCUMask(st, (uint32_t)words, mask);
+    }
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, side_prio(least, greatest));
+}
+
 inline SideStreams* side_streams() {
     static SideStreams streams[64];
     static std::mutex init_mu;
@@ -3322,8 +3346,7 @@ inline SideStreams* side_streams() {
         for (int i = 0; i < SideStreams::kN; ++i)
             if ((!ss.fork[i] && hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming)) ||
                 (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
-                (!ss.st[i] && hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking,
-                                                          greatest)))
+                (!ss.st[i] && side_stream_create(&ss.st[i], least, greatest)))
                 return nullptr;
         if (hipEventCreateWithFlags(&ss.cand, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
