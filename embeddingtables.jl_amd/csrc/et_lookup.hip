@@ -497,6 +497,8 @@ struct StripeMap {
     uint32_t ntload_mask;  // bit t: non-temporal row loads for table t
     uint32_t prio_mask;    // bit t: table t's waves run at raised issue priority
     int prio;
+    int nheavy;            // entry[x][0, nheavy): the heavy tables (> light_bytes)
+    int qorder;            // queued schedule: 1 = every heavy item before the light ones
 };
 
 template <typename T, typename A, int D, int U, bool NT, bool NTI, bool SG = false>
@@ -610,10 +612,24 @@ __global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, Stri
     }
     __syncthreads();
     const uint32_t it = s_item;
-    if (it != ~0u)
+    if (it != ~0u) {
+        int64_t slot = (int64_t)(it % per);
+        if (sm.qorder == 1 && sm.nheavy > 0 && sm.nheavy < ntables) {
+            // heavy-first: the queue's first nheavy * stripe_chunks items are the heavy
+            // tables' chunks, then the light ones (slot = j * ntables + k, as the static order)
+            const int64_t hn = (int64_t)sm.nheavy * stripe_chunks;
+            const int nl = ntables - sm.nheavy;
+            slot = slot < hn ? (slot / sm.nheavy) * ntables + slot % sm.nheavy
+                             : ((slot - hn) / nl) * ntables + sm.nheavy + (slot - hn) % nl;
+        } else if (sm.qorder == 2 && sm.nheavy > 0 && sm.nheavy < ntables) {  // light first
+            const int nl = ntables - sm.nheavy;
+            const int64_t ln = (int64_t)nl * stripe_chunks;
+            slot = slot < ln ? (slot / nl) * ntables + sm.nheavy + slot % nl
+                             : ((slot - ln) / sm.nheavy) * ntables + (slot - ln) % sm.nheavy;
+        }
         striped_body<T, A, D, U, NT, false, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
-                                                stripe_chunks, nchunks, (int)(it / per),
-                                                (int64_t)(it % per));
+                                                stripe_chunks, nchunks, (int)(it / per), slot);
+    }
     if (threadIdx.x == 0 && atomicAdd(&q.done, 1u) == gridDim.x - 1u) {  // the last one
         for (int x = 0; x < kXcds; ++x) atomicExch(&q.head[x], 0u);
         atomicExch(&q.done, 0u);
@@ -808,6 +824,7 @@ struct LookupTuning {
     int sgpr = 1;                  // ET_SGPR=0: 512-byte rows use the per-lane loop too
     int sg256 = 0;                 // ET_SG256=1: 256-byte rows take the scalar loop too
     int heavy_prio = 0;            // ET_HEAVY_PRIO=1: heavy tables' waves at priority 2
+    int qorder = 0;                // ET_QORDER=1: queued schedule, heavy items first
 };
 
 inline const LookupTuning& tuning() {
@@ -827,6 +844,7 @@ inline const LookupTuning& tuning() {
         if (const char* e = getenv("ET_SGPR")) v.sgpr = atoi(e);
         if (const char* e = getenv("ET_SG256")) v.sg256 = atoi(e);
         if (const char* e = getenv("ET_HEAVY_PRIO")) v.heavy_prio = atoi(e);
+        if (const char* e = getenv("ET_QORDER")) v.qorder = atoi(e);
         return v;
     }();
     return t;
@@ -843,6 +861,7 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
     int64_t bytes[ET_MAX_TABLES_PER_LAUNCH];
     sm.ntload_mask = 0;
     sm.prio_mask = 0;
+    sm.qorder = tu.qorder;
     for (int t = 0; t < n; ++t) {
         bytes[t] = pack.d[t].nrows * pack.d[t].ld_table * es;
         if (bytes[t] > tu.light_bytes) {
@@ -866,6 +885,7 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
     int cnt[kXcds] = {0};
     for (int x = 0; x < kXcds; ++x)
         for (int h = 0; h < nh; ++h) sm.entry[x][cnt[x]++] = (uint32_t)heavy[h] | ((uint32_t)x << 8);
+    sm.nheavy = nh;
     // linear list of light stripes (order[i], st), st < kXcds; XCD x takes [x*nl, (x+1)*nl)
     for (int q = 0; q < nl * kXcds; ++q) {
         const int x = q / (nl > 0 ? nl : 1);
