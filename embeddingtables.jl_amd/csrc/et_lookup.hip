@@ -265,6 +265,38 @@ __device__ __forceinline__ void run_bags(const et_lookup_desc& d, int64_t batch,
     }
 }
 
+// A feature slice of a bag range (the feature-split tables of the striped schedule): the
+// bags [bag0, bag1) of table d, features [fofs, fofs + DS) only — DS-feature rows at the
+// table's row stride, so each lane group reads DS * sizeof(T) bytes per row.  Sums are per
+// feature in pool order, exactly as run_bags, so the output is bit-identical however the
+// features are cut.
+template <typename T, typename A, int DS, bool NT>
+__device__ __forceinline__ void run_bags_slice(const et_lookup_desc& d, int64_t batch,
+                                               T* __restrict__ dst, int64_t ld_dst, int64_t bag0,
+                                               int64_t bag1, int fofs) {
+    using G = VecGeom<T, DS>;
+    const T* table = reinterpret_cast<const T*>(d.table) + fofs;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / G::LPR, sub = lane % G::LPR;
+    const int64_t per_round = 4 * G::GPW;
+    const int pool = d.pool;
+    const int cnt0 = pool < G::LPR ? pool : G::LPR;
+    const uint32_t ldt = (uint32_t)d.ld_table, nr = (uint32_t)d.nrows;
+    const int64_t end = bag1 < batch ? bag1 : batch;
+    int64_t bag = bag0 + wave * G::GPW + g;
+    long long my_next = load_idx_chunk<G::LPR>(d.idx + (bag < end ? bag : end - 1) * d.ld_idx,
+                                                cnt0, sub);
+    while (bag < end) {
+        const long long my = my_next;
+        const int64_t nbag = bag + per_round;
+        if (nbag < end) my_next = load_idx_chunk<G::LPR>(d.idx + nbag * d.ld_idx, cnt0, sub);
+        bag_sum_vec<T, A, DS, G::U, NT, false>(table, ldt, nr, 0u, d.idx + bag * d.ld_idx, pool,
+                                               my, dst + bag * ld_dst + d.dst_row_off + fofs, g,
+                                               sub, G::VPR);
+        bag = nbag;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Scalar-addressed bag loop for 512-byte rows (D = 128 fp32, 256 f16 / bf16, 64 f64 /
 // i64): LPR = 32, so a wave holds two bags — A in lanes 0-31, B in lanes 32-63 — and
@@ -492,8 +524,13 @@ constexpr int kXcds = 8;
 
 // 32-bit entries (table | stripe << 8) so the map is read with scalar loads (gfx950
 // has no scalar byte loads).
+constexpr int kMaxStripeEntries = 40;  // per XCD (kernel-argument size bound)
 struct StripeMap {
-    uint32_t entry[kXcds][ET_MAX_TABLES_PER_LAUNCH];
+    // entry[x][k]: table (bits 0-7), stripe (8-15), feature group + 1 (16-23; 0: whole
+    // rows); every XCD has nent entries (the feature-split tables take fsplit_g each)
+    uint32_t entry[kXcds][kMaxStripeEntries];
+    int nent;
+    int fsplit_g;          // feature groups of a split table (2, 4 or 8)
     uint32_t ntload_mask;  // bit t: non-temporal row loads for table t
     uint32_t prio_mask;    // bit t: table t's waves run at raised issue priority
     int prio;
@@ -511,9 +548,23 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
     const int64_t j = slot / ntables;
     const uint32_t e = sm.entry[x][k];
     const int t = (int)(e & 0xff);
-    const int64_t chunk = (int64_t)(e >> 8) * stripe_chunks + j;
+    const int64_t chunk = (int64_t)((e >> 8) & 0xff) * stripe_chunks + j;
     if (j >= stripe_chunks || chunk >= nchunks) return;
     if ((sm.prio_mask >> t) & 1u) __builtin_amdgcn_s_setprio(2);
+    if constexpr (D == 128 && sizeof(T) == 4) {
+        const uint32_t fg = e >> 16;
+        if (fg != 0u) {  // a feature slice of a split table (build_stripe_map)
+            const int64_t per_round = SG ? 8 : 4 * VecGeom<T, D>::GPW;
+            const int64_t b0 = chunk * per_round * rounds, b1 = b0 + per_round * rounds;
+            const int fofs = (int)(fg - 1u) * (D / sm.fsplit_g);
+            switch (sm.fsplit_g) {
+                case 2: run_bags_slice<T, A, D / 2, NT>(pack.d[t], batch, dst, ld_dst, b0, b1, fofs); break;
+                case 8: run_bags_slice<T, A, D / 8, NT>(pack.d[t], batch, dst, ld_dst, b0, b1, fofs); break;
+                default: run_bags_slice<T, A, D / 4, NT>(pack.d[t], batch, dst, ld_dst, b0, b1, fofs); break;
+            }
+            return;
+        }
+    }
     if constexpr (SG) {
         if ((sm.ntload_mask >> t) & 1u)
             run_bags_s<T, A, U, NT, true, sg_bpl<T>(D)>(pack.d[t], batch, dst, ld_dst, chunk,
@@ -825,6 +876,10 @@ struct LookupTuning {
     int sg256 = 0;                 // ET_SG256=1: 256-byte rows take the scalar loop too
     int heavy_prio = 0;            // ET_HEAVY_PRIO=1: heavy tables' waves at priority 2
     int qorder = 0;                // ET_QORDER=1: queued schedule, heavy items first
+    // Tables of (light_bytes, fsplit_bytes] cut into fsplit_g feature groups, group g on XCDs
+    // [g * 8 / G, (g + 1) * 8 / G), so each XCD's L2 holds 1/G of the table (ET_FSPLIT_*)
+    int64_t fsplit_bytes = 0;
+    int fsplit_g = 4;
 };
 
 inline const LookupTuning& tuning() {
@@ -845,6 +900,11 @@ inline const LookupTuning& tuning() {
         if (const char* e = getenv("ET_SG256")) v.sg256 = atoi(e);
         if (const char* e = getenv("ET_HEAVY_PRIO")) v.heavy_prio = atoi(e);
         if (const char* e = getenv("ET_QORDER")) v.qorder = atoi(e);
+        if (const char* e = getenv("ET_FSPLIT_BYTES")) v.fsplit_bytes = atoll(e);
+        if (const char* e = getenv("ET_FSPLIT_G")) {
+            const int g = atoi(e);
+            v.fsplit_g = g == 2 || g == 8 ? g : 4;
+        }
         return v;
     }();
     return t;
@@ -854,17 +914,24 @@ int max_rounds() { return tuning().max_rounds; }
 
 // Stripe assignment: heavy tables -> stripe x on XCD x; light tables' stripes laid out
 // table after table (alternating large and small tables) and cut into kXcds equal runs.
-inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& sm) {
+inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& sm,
+                             bool can_split = false) {
     const LookupTuning& tu = tuning();
     int heavy[ET_MAX_TABLES_PER_LAUNCH], light[ET_MAX_TABLES_PER_LAUNCH];
-    int nh = 0, nl = 0;
+    int split[ET_MAX_TABLES_PER_LAUNCH];
+    int nh = 0, nl = 0, nsp = 0;
     int64_t bytes[ET_MAX_TABLES_PER_LAUNCH];
     sm.ntload_mask = 0;
     sm.prio_mask = 0;
     sm.qorder = tu.qorder;
+    sm.fsplit_g = tu.fsplit_g;
     for (int t = 0; t < n; ++t) {
         bytes[t] = pack.d[t].nrows * pack.d[t].ld_table * es;
-        if (bytes[t] > tu.light_bytes) {
+        if (can_split && bytes[t] > tu.light_bytes && bytes[t] <= tu.fsplit_bytes &&
+            pack.d[t].cols_per_page == 0 && pack.d[t].dim == 128 &&
+            n + (nsp + 1) * (tu.fsplit_g - 1) <= kMaxStripeEntries) {
+            split[nsp++] = t;
+        } else if (bytes[t] > tu.light_bytes) {
             heavy[nh++] = t;
             if (tu.heavy_prio) sm.prio_mask |= 1u << t;
             if (tu.ntload && bytes[t] > tu.ntload_bytes) sm.ntload_mask |= 1u << t;
@@ -885,12 +952,22 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
     int cnt[kXcds] = {0};
     for (int x = 0; x < kXcds; ++x)
         for (int h = 0; h < nh; ++h) sm.entry[x][cnt[x]++] = (uint32_t)heavy[h] | ((uint32_t)x << 8);
-    sm.nheavy = nh;
+    // split tables: XCD x serves feature group g = x / P (P = 8 / G XCDs per group) over the
+    // stripes G * (x % P) .. G * (x % P) + G - 1, so every group covers all 8 stripes
+    const int G = sm.fsplit_g, P = kXcds / G;
+    for (int x = 0; x < kXcds; ++x)
+        for (int q = 0; q < nsp; ++q)
+            for (int m = 0; m < G; ++m)
+                sm.entry[x][cnt[x]++] = (uint32_t)split[q] |
+                                        ((uint32_t)(G * (x % P) + m) << 8) |
+                                        ((uint32_t)(x / P + 1) << 16);
+    sm.nheavy = nh + nsp * G;
     // linear list of light stripes (order[i], st), st < kXcds; XCD x takes [x*nl, (x+1)*nl)
     for (int q = 0; q < nl * kXcds; ++q) {
         const int x = q / (nl > 0 ? nl : 1);
         sm.entry[x][cnt[x]++] = (uint32_t)order[q / kXcds] | ((uint32_t)(q % kXcds) << 8);
     }
+    sm.nent = cnt[0];
 }
 
 template <typename T, typename A, int D, int U, bool NT, bool PG = false, bool MK = false>
@@ -928,16 +1005,17 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     if (nchunks <= 0) return ET_OK;
     if (!PG && !MK && n > 1 && tuning().striped) {
         StripeMap sm;
-        build_stripe_map(pack, n, (int)sizeof(T), sm);
+        build_stripe_map(pack, n, (int)sizeof(T), sm, D == 128 && sizeof(T) == 4);
+        const int ne = sm.nent;  // entries per XCD (n, plus fsplit_g - 1 per split table)
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
-        const int64_t grid = (int64_t)kXcds * n * stripe_chunks;
+        const int64_t grid = (int64_t)kXcds * ne * stripe_chunks;
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
         const int qslot = tuning().queued ? xcd_queue_slot(s) : -1;
         if (qslot >= 0 && grid < 0xffffffffll) {
             if constexpr (kSG) {
                 if (sg) {
                     hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, true>),
-                                       dim3((unsigned)grid), dim3(256), 0, s, pack, sm, n, batch,
+                                       dim3((unsigned)grid), dim3(256), 0, s, pack, sm, ne, batch,
                                        reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
                                        nchunks, qslot);
                     ET_LAUNCH_CHECK("k_pooled_vec_queued");
@@ -945,7 +1023,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
                 }
             }
             hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, false>), dim3((unsigned)grid),
-                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
                                ld_dst, rounds, stripe_chunks, nchunks, qslot);
             ET_LAUNCH_CHECK("k_pooled_vec_queued");
             return ET_OK;
@@ -953,7 +1031,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         if constexpr (kSG) {
             if (sg && tuning().w8) {
                 hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT, false, true>),
-                                   dim3((unsigned)grid), dim3(256), 0, s, pack, sm, n, batch,
+                                   dim3((unsigned)grid), dim3(256), 0, s, pack, sm, ne, batch,
                                    reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
                                    nchunks);
                 ET_LAUNCH_CHECK("k_pooled_vec_striped");
@@ -961,7 +1039,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
             }
             if (sg) {
                 hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT, false, true>),
-                                   dim3((unsigned)grid), dim3(256), 0, s, pack, sm, n, batch,
+                                   dim3((unsigned)grid), dim3(256), 0, s, pack, sm, ne, batch,
                                    reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
                                    nchunks);
                 ET_LAUNCH_CHECK("k_pooled_vec_striped");
@@ -970,15 +1048,15 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         }
         if (tuning().w8 && D == 128 && __is_same(T, float))
             hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT>), dim3((unsigned)grid),
-                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
                                ld_dst, rounds, stripe_chunks, nchunks);
         else if (tuning().ntidx && D == 128 && __is_same(T, float))
             hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT, true>), dim3((unsigned)grid),
-                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
                                ld_dst, rounds, stripe_chunks, nchunks);
         else
             hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT>), dim3((unsigned)grid),
-                               dim3(256), 0, s, pack, sm, n, batch, reinterpret_cast<T*>(dst),
+                               dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
                                ld_dst, rounds, stripe_chunks, nchunks);
         ET_LAUNCH_CHECK("k_pooled_vec_striped");
         return ET_OK;
