@@ -2727,8 +2727,15 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
 // over the single-chunk columns (k_sgd_exact) — the plan is off the update's critical path.
 inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, const Grouped& out, hipStream_t s,
-                             uint32_t ec_mask, const EhMap& eh, hipEvent_t cand_ready) {
+                             uint32_t ec_mask, const EhMap& eh, hipEvent_t cand_ready,
+                             hipEvent_t gate = nullptr, int gate_at = 0) {
     if (eh.mask) ET_HIP_CHECK(hipStreamWaitEvent(s, cand_ready, 0));  // k_eh_pick's candidates
+    // gate (ET_PLAN_GATE experiments): recorded after plan step gate_at (1: k_chain_tiles,
+    // 2: k_chain_plan, 3: k_chain_emit) for the caller's stream to wait on
+    auto mark = [&](int at) -> int {
+        if (gate && gate_at == at) ET_HIP_CHECK(hipEventRecord(gate, s));
+        return ET_OK;
+    };
     const int64_t mmax = n / chunk + 2;
     const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
     const int64_t tmax = chain_tiles_max(n, chunk);
@@ -2736,6 +2743,7 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask, eh,
                        w.eh_cand, out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
                        w.chain_tile_col);
+    if (mark(1) != ET_OK) return ET_ERR_HIP;
     const bool s1 = chain_fed(kFedRegular);  // S = 1 plans: entries = occurrences, no run counts
     if (!s1)
         hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
@@ -2748,6 +2756,7 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
                        s1 ? 0 : 4 | (int)lat_reg << 8);
     hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
                        w.chain_info, w.chain_e0, w.chain_order);
+    if (mark(2) != ET_OK) return ET_ERR_HIP;
     if (s1)
         hipLaunchKernelGGL(k_chain_emit1, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                            out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
@@ -2759,6 +2768,7 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
                            w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
                            w.chain_ent, w.chains);
     ET_LAUNCH_CHECK("k_chain_emit");
+    if (mark(3) != ET_OK) return ET_ERR_HIP;
     static const bool check = [] {
         const char* e = getenv("ET_CHAIN_CHECK");
         return e && atoi(e) != 0;
@@ -3307,6 +3317,7 @@ struct SideStreams {
     hipStream_t st[kN] = {nullptr, nullptr, nullptr};
     hipEvent_t fork[kN] = {nullptr, nullptr, nullptr}, join[kN] = {nullptr, nullptr, nullptr};
     hipEvent_t cand = nullptr;  // the hot-column candidates are picked (k_eh_pick)
+    hipEvent_t gate = nullptr;  // ET_PLAN_GATE: a step of the regular plan is done
 };
 
 // The side streams' priority: the device's greatest (default), or ET_SIDE_PRIO=0 the
@@ -3348,6 +3359,7 @@ inline SideStreams* side_streams() {
                 (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
                 (!ss.st[i] && side_stream_create(&ss.st[i], least, greatest)))
                 return nullptr;
+        if (hipEventCreateWithFlags(&ss.gate, hipEventDisableTiming) != hipSuccess) return nullptr;
         if (hipEventCreateWithFlags(&ss.cand, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
     return &ss;
@@ -3612,9 +3624,16 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
         cr.side = fork.fork(1);  // after the index phase's chunk records (and the plan)
         if (!cr.side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
         if (!apply_only && plan_side) {
+            // ET_PLAN_GATE=1/2/3 (experiments): the chunk pass waits for the plan's
+            // k_chain_tiles / k_chain_plan / k_chain_emit, whose single-workgroup kernels
+            // otherwise wait for CUs held by the chunk pass's persistent workgroups
+            static const int gate_at = (int)et::env_uint("ET_PLAN_GATE", 0u);
             rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, cr.side,
-                                       use_ec ? ec.mask : 0u, ehm, sides->cand);
+                                       use_ec ? ec.mask : 0u, ehm, sides->cand, sides->gate,
+                                       gate_at);
             if (rc != ET_OK) return rc;
+            if (gate_at >= 1 && gate_at <= 3)
+                ET_HIP_CHECK(hipStreamWaitEvent(s, sides->gate, 0));
         }
     }
     if (index_only) return ET_OK;

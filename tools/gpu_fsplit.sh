@@ -11,3 +11,7 @@ for r in 1 2; do for v in "ET_X=0" "ET_FSPLIT_BYTES=16777216 ET_FSPLIT_G=4" "ET_
   env $v timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-extra --cpu-seconds 0 > $OUT/bench_q.txt 2>&1 || { echo BENCH_FAIL $v; tail -5 $OUT/bench_q.txt; exit 1; }
   echo "$v $(tail -1 $OUT/bench_q.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["roofline"]["frac"])')"
 done; done
+for r in 1 2; do for v in "ET_PLAN_GATE=0" "ET_PLAN_GATE=1" "ET_PLAN_GATE=2" "ET_PLAN_GATE=3"; do
+  env $v timeout -k 10 200 python3 tools/exact_cfg4.py exact > $OUT/cfg4.txt 2>&1 || { echo CFG4_FAIL $v; tail -5 $OUT/cfg4.txt; exit 1; }
+  echo "$v $(tail -1 $OUT/cfg4.txt)"
+done; done
