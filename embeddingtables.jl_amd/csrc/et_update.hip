@@ -2908,6 +2908,9 @@ inline bool sgd_chunks_occ5() {
 // and their column count, the side stream of the regular chains (forked from the caller's
 // stream after the index phase).
 struct ChainRun {
+    // reset[i]: the chain list's item counter is reset (early, regular, hot; for tail
+    // launches on the caller's stream after the chunk pass)
+    hipEvent_t reset[3] = {nullptr, nullptr, nullptr};
     hipStream_t ec_side = nullptr;
     uint32_t ec_ncols = 0;
     hipStream_t eh_side = nullptr;  // the early hot columns (ET_EH)
@@ -2921,7 +2924,7 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
                   const uint32_t* order, const uint2* info, const uint32_t* nocc,
                   const uint32_t* ent, int ns, float eta32, double eta64, unsigned nhf,
                   unsigned nb, hipStream_t s, bool excl = false, bool fed = false,
-                  uint32_t lds_req = 0u) {
+                  uint32_t lds_req = 0u, hipEvent_t reset_ev = nullptr, bool tail = false) {
     static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++;
         // experiments: ET_CHAIN_QUAD=0 walks S = 1 chains with the 64-feature asm loop
         const char* e = getenv("ET_CHAIN_ASM");
@@ -2948,13 +2951,19 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     ET_HIP_CHECK(attr_x);
     // plain items start past the helper-fed ones (at 0 when no workgroup is helper-fed);
-    // the helper-fed counter at 0
-    if (nhf > 0)
-        ET_HIP_CHECK(hipMemcpyAsync(counters + kCntNext, counters + kCntHfItems, 4,
-                                    hipMemcpyDeviceToDevice, s));
-    else
-        ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
-    ET_HIP_CHECK(hipMemsetAsync(counters + kCntHfNext, 0, 4, s));
+    // the helper-fed counter at 0.  A tail launch (more workgroups on the same list, taking
+    // items from the same counter) resets nothing; reset_ev marks the reset for it.
+    if (tail) {
+        if (fed || nhf > 0) return ET_OK;
+    } else {
+        if (nhf > 0)
+            ET_HIP_CHECK(hipMemcpyAsync(counters + kCntNext, counters + kCntHfItems, 4,
+                                        hipMemcpyDeviceToDevice, s));
+        else
+            ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
+        ET_HIP_CHECK(hipMemsetAsync(counters + kCntHfNext, 0, 4, s));
+        if (reset_ev) ET_HIP_CHECK(hipEventRecord(reset_ev, s));
+    }
     if (fed) {  // every chain planned at S = 1: the fed walk
         static const hipError_t attr_f = hipFuncSetAttribute(
             reinterpret_cast<const void*>(&k_sgd_chains_fed<MODE, NT>),
@@ -3024,7 +3033,8 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         const unsigned hf_wg = 0u;
         rc = launch_chains<MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
                                      w.ec.info, w.ec.nocc, w.ec.ent, ns, eta32, eta64, hf_wg, eb,
-                                     cr.ec_side, (excl & 1u) != 0, chain_fed(kFedEarly));
+                                     cr.ec_side, (excl & 1u) != 0, chain_fed(kFedEarly), 0u,
+                                     cr.reset[0]);
         if (rc != ET_OK) return rc;
     }
     if (cr.eh_side) {
@@ -3037,12 +3047,13 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
         rc = launch_chains<MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
                                      w.eh.info, w.eh.nocc, w.eh.ent, ns, eta32, eta64, 0u, eb,
                                      cr.eh_side, (excl & 4u) != 0, chain_fed(kFedHot),
-                                     eh_lds <= 160u * 1024u ? eh_lds : 0u);
+                                     eh_lds <= 160u * 1024u ? eh_lds : 0u, cr.reset[2]);
         if (rc != ET_OK) return rc;
     }
     rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
                                  w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u, reg_wg,
-                                 cr.side, (excl & 2u) != 0, chain_fed(kFedRegular));
+                                 cr.side, (excl & 2u) != 0, chain_fed(kFedRegular), 0u,
+                                 cr.reset[1]);
     if (rc != ET_OK) return rc;
 #define ET_SGD_EXACT(DD)                                                                       \
     case DD:                                                                                   \
@@ -3070,6 +3081,33 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                            0, s, pack, ntables, gr.keys, gr.vals, w.recs, w.counters, w.partials,
                            pdim, sent, eta32, eta64, 1);
         ET_LAUNCH_CHECK("k_sgd_chunks_generic");
+    }
+    // Tail workgroups (ET_TAIL_EC / _EH / _REG, experiments): more workgroups for a chain
+    // list on the caller's stream, so they start when the chunk pass ends and take the
+    // list's remaining items from the same counter (the CUs the pass held are idle then)
+    static const unsigned tail_ec = env_uint("ET_TAIL_EC", 0u), tail_eh = env_uint("ET_TAIL_EH", 0u),
+                          tail_reg = env_uint("ET_TAIL_REG", 0u);
+    if (cr.ec_side && tail_ec && cr.reset[0]) {
+        ET_HIP_CHECK(hipStreamWaitEvent(s, cr.reset[0], 0));
+        rc = launch_chains<MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
+                                     w.ec.info, w.ec.nocc, w.ec.ent, ns, eta32, eta64, 0u, tail_ec,
+                                     s, (excl & 1u) != 0, chain_fed(kFedEarly), 0u, nullptr, true);
+        if (rc != ET_OK) return rc;
+    }
+    if (cr.eh_side && tail_eh && cr.reset[2]) {
+        ET_HIP_CHECK(hipStreamWaitEvent(s, cr.reset[2], 0));
+        rc = launch_chains<MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
+                                     w.eh.info, w.eh.nocc, w.eh.ent, ns, eta32, eta64, 0u, tail_eh,
+                                     s, (excl & 4u) != 0, chain_fed(kFedHot), 0u, nullptr, true);
+        if (rc != ET_OK) return rc;
+    }
+    if (tail_reg && cr.reset[1]) {
+        ET_HIP_CHECK(hipStreamWaitEvent(s, cr.reset[1], 0));
+        rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
+                                     w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u,
+                                     tail_reg, s, (excl & 2u) != 0, chain_fed(kFedRegular), 0u,
+                                     nullptr, true);
+        if (rc != ET_OK) return rc;
     }
     return ET_OK;
 }
@@ -3318,6 +3356,7 @@ struct SideStreams {
     hipEvent_t fork[kN] = {nullptr, nullptr, nullptr}, join[kN] = {nullptr, nullptr, nullptr};
     hipEvent_t cand = nullptr;  // the hot-column candidates are picked (k_eh_pick)
     hipEvent_t gate = nullptr;  // ET_PLAN_GATE: a step of the regular plan is done
+    hipEvent_t reset[kN] = {nullptr, nullptr, nullptr};  // a chain list's counter is reset
 };
 
 // The side streams' priority: the device's greatest (default), or ET_SIDE_PRIO=0 the
@@ -3360,6 +3399,9 @@ inline SideStreams* side_streams() {
                 (!ss.st[i] && side_stream_create(&ss.st[i], least, greatest)))
                 return nullptr;
         if (hipEventCreateWithFlags(&ss.gate, hipEventDisableTiming) != hipSuccess) return nullptr;
+        for (int i = 0; i < SideStreams::kN; ++i)
+            if (!ss.reset[i] && hipEventCreateWithFlags(&ss.reset[i], hipEventDisableTiming) != hipSuccess)
+                return nullptr;
         if (hipEventCreateWithFlags(&ss.cand, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
     return &ss;
@@ -3605,6 +3647,8 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     }
     et::ChainRun cr;
     if (chain) {
+        if (sides)
+            for (int i = 0; i < 3; ++i) cr.reset[i] = sides->reset[i];
         cr.ec_side = ec_side;
         cr.ec_ncols = use_ec ? ec.col0[ec.n] : 0u;
         cr.eh_side = eh_side;

@@ -15,3 +15,7 @@ for r in 1 2; do for v in "ET_PLAN_GATE=0" "ET_PLAN_GATE=1" "ET_PLAN_GATE=2" "ET
   env $v timeout -k 10 200 python3 tools/exact_cfg4.py exact > $OUT/cfg4.txt 2>&1 || { echo CFG4_FAIL $v; tail -5 $OUT/cfg4.txt; exit 1; }
   echo "$v $(tail -1 $OUT/cfg4.txt)"
 done; done
+for r in 1 2; do for v in "ET_CHAIN_LDS=40" "ET_CHAIN_LDS=40 ET_CHAIN_WG=256" "ET_CHAIN_LDS=20 ET_CHAIN_WG=384"; do
+  env $v timeout -k 10 200 python3 tools/exact_cfg4.py exact > $OUT/cfg4.txt 2>&1 || { echo CFG4_FAIL $v; tail -5 $OUT/cfg4.txt; exit 1; }
+  echo "$v $(tail -1 $OUT/cfg4.txt)"
+done; done
