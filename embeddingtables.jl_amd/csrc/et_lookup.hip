@@ -61,12 +61,18 @@ __device__ __forceinline__ u32x4 pack16(const T (&x)[N]) {
 }
 
 // Broadcast the 64-bit value held by lane (g*LPR + i) to every lane of group g; i is
-// wave-uniform.  With <= 4 groups per wave this is 2*GPW v_readlane + selects (no LDS
-// round trip, nothing for the waitcnt pass to serialise); wider waves use ds_bpermute.
+// wave-uniform.  With <= ET_BCAST_READLANE_MAX_GPW groups per wave this is 2*GPW
+// v_readlane + selects (no LDS round trip, nothing for the waitcnt pass to serialise);
+// wider waves use ds_bpermute.  Round 4: 2 (four groups — 256-byte rows, the Float16
+// config-3 leg — take ds_bpermute: 14 VALU per row were the issue bound of its
+// L2-resident tables); -DET_BCAST_READLANE_MAX_GPW=4 restores the round-3 choice.
+#ifndef ET_BCAST_READLANE_MAX_GPW
+#define ET_BCAST_READLANE_MAX_GPW 2
+#endif
 template <int LPR>
 __device__ __forceinline__ long long group_bcast(long long v, int i, int g) {
     constexpr int GPW = 64 / LPR;
-    if constexpr (GPW <= 4) {
+    if constexpr (GPW <= ET_BCAST_READLANE_MAX_GPW) {
         const int lo = (int)v, hi = (int)(v >> 32);
         int rlo = __builtin_amdgcn_readlane(lo, i), rhi = __builtin_amdgcn_readlane(hi, i);
 #pragma unroll
