@@ -88,6 +88,30 @@ __device__ __forceinline__ long long group_bcast(long long v, int i, int g) {
     }
 }
 
+// The same for a 32-bit value (one readlane per group, or one ds_bpermute).
+template <int LPR>
+__device__ __forceinline__ uint32_t group_bcast32(uint32_t v, int i, int g) {
+    constexpr int GPW = 64 / LPR;
+    if constexpr (GPW <= ET_BCAST_READLANE_MAX_GPW) {
+        int r = __builtin_amdgcn_readlane((int)v, i);
+#pragma unroll
+        for (int gg = 1; gg < GPW; ++gg) {
+            const int t = __builtin_amdgcn_readlane((int)v, gg * LPR + i);
+            r = g == gg ? t : r;
+        }
+        return (uint32_t)r;
+    } else {
+        return (uint32_t)__shfl((int)v, g * LPR + i, 64);
+    }
+}
+
+// A lane's 1-based index as its 0-based row, or ~0 when out of range (checked once per
+// index, before the broadcast, instead of once per row in every lane of its group).
+__device__ __forceinline__ uint32_t idx_row32(long long v, uint32_t nrows) {
+    const uint64_t row = (uint64_t)(v - 1);
+    return row < (uint64_t)nrows ? (uint32_t)row : ~0u;
+}
+
 // The first (up to) LPR indices of a bag, one per lane of the group; lanes past the
 // end re-read the last one so that no lane is masked off.
 template <int LPR, bool NTI = false>
@@ -115,7 +139,7 @@ __device__ __forceinline__ long long load_idx_chunk(const int64_t* __restrict__ 
 // re-read its last vector (same cache line, never out of bounds) and never store.
 template <typename T, typename A, int D, int UU, bool NTL, bool PG = false, bool MK = false>
 __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t ld_table,
-                                         uint32_t nrows, uint32_t cpp, long long my, int g,
+                                         uint32_t nrows, uint32_t cpp, uint32_t myr, int g,
                                          int sub, int i0, bool first_batch,
                                          A (&acc)[VecGeom<T, D>::NV][VecGeom<T, D>::N],
                                          int& bad, int vpr) {
@@ -126,10 +150,9 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t l
     const T* base[UU];
 #pragma unroll
     for (int u = 0; u < UU; ++u) {
-        const long long r = group_bcast<LPR>(my, i0 + u, g);
-        const uint64_t row = (uint64_t)(r - 1);
-        ok[u] = row < (uint64_t)nrows;
-        const uint32_t row32 = ok[u] ? (uint32_t)row : 0u;
+        const uint32_t r = group_bcast32<LPR>(myr, i0 + u, g);  // idx_row32 of the index
+        ok[u] = r != ~0u;
+        const uint32_t row32 = ok[u] ? r : 0u;
         if constexpr (PG) {
             const uint32_t page = row32 / cpp;
             off[u] = (uint64_t)(row32 - page * cpp) * ld_table;
@@ -201,9 +224,10 @@ __device__ __forceinline__ void bag_sum_vec(const T* __restrict__ table, uint32_
     for (int c0 = 0; c0 < pool; c0 += LPR) {
         const int cnt = pool - c0 < LPR ? pool - c0 : LPR;
         const long long my = c0 == 0 ? my0 : load_idx_chunk<LPR>(ip + c0, cnt, sub);
+        const uint32_t myr = idx_row32(my, nrows);
         int i0 = 0;
 #define ET_LOAD_ADD(UU) \
-    load_add<T, A, D, UU, NTL, PG, MK>(table, ld_table, nrows, cpp, my, g, sub, i0,        \
+    load_add<T, A, D, UU, NTL, PG, MK>(table, ld_table, nrows, cpp, myr, g, sub, i0,       \
                                        c0 + i0 == 0, acc, bad, vpr)
         for (; i0 + U <= cnt; i0 += U) ET_LOAD_ADD(U);
         if constexpr (U > 8) {
