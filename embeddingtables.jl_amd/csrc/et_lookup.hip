@@ -19,6 +19,7 @@
 //     `_divrem_index(k, ntables)` work queue (src/lookup.jl:351-355);
 //   * descriptors travel by value in the kernel-argument segment (no device
 //     allocation, hipGraph-capturable).
+#include <type_traits>
 #include "et_common.h"
 
 #include <stdlib.h>
@@ -180,21 +181,38 @@ __device__ __forceinline__ void load_add(const T* __restrict__ table, uint32_t l
                 buf[u][v] = src[vix[v]];
         }
     }
+    // Out-of-range rows (loaded from row 0) add zeros.  They are rare, so the wave tests
+    // the batch once and only a batch holding one pays the per-row zero selects (round 4:
+    // four selects per 16-byte vector and row were a tenth of the L2-resident tables' VALU).
+    int anybad = 0;
 #pragma unroll
-    for (int u = 0; u < UU; ++u) {
-        bad += ok[u] ? 0 : 1;
+    for (int u = 0; u < UU; ++u) anybad |= ok[u] ? 0 : 1;
+    auto add_rows = [&](auto checked) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            T x[N];
-            unpack16<T, N>(ok[u] ? buf[u][v] : u32x4{0u, 0u, 0u, 0u}, x);
+        for (int u = 0; u < UU; ++u) {
 #pragma unroll
-            for (int k = 0; k < N; ++k) {
-                if (u == 0)
-                    acc[v][k] = first_batch ? A(x[k]) : A(acc[v][k] + A(x[k]));
+            for (int v = 0; v < NV; ++v) {
+                T x[N];
+                if constexpr (decltype(checked)::value)
+                    unpack16<T, N>(ok[u] ? buf[u][v] : u32x4{0u, 0u, 0u, 0u}, x);
                 else
-                    acc[v][k] = A(acc[v][k] + A(x[k]));
+                    unpack16<T, N>(buf[u][v], x);
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    if (u == 0)
+                        acc[v][k] = first_batch ? A(x[k]) : A(acc[v][k] + A(x[k]));
+                    else
+                        acc[v][k] = A(acc[v][k] + A(x[k]));
+                }
             }
         }
+    };
+    if (__builtin_expect(__any(anybad), 0)) {
+#pragma unroll
+        for (int u = 0; u < UU; ++u) bad += ok[u] ? 0 : 1;
+        add_rows(std::true_type{});
+    } else {
+        add_rows(std::false_type{});
     }
 }
 
