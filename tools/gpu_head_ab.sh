@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 4: headline A/B, the final lookup vs the build before the feature-split change.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/headab; mkdir -p $OUT
+ALT=$PWD/tools/alt/libembtab_hip_alt.so
+for r in 1 2 3; do for v in "ET_X=0" "ET_LIBRARY=$ALT"; do
+  env $v timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-extra --cpu-seconds 0 > $OUT/b.txt 2>&1 || { echo BENCH_FAIL $v; tail -5 $OUT/b.txt; exit 1; }
+  echo "${v##*/} $(tail -1 $OUT/b.txt | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["roofline"]["frac"])')"
+done; done
