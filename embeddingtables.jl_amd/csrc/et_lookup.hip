@@ -599,6 +599,9 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
     const int64_t chunk = (int64_t)((e >> 8) & 0xff) * stripe_chunks + j;
     if (j >= stripe_chunks || chunk >= nchunks) return;
     if ((sm.prio_mask >> t) & 1u) __builtin_amdgcn_s_setprio(2);
+#ifdef ET_FSPLIT
+    // Feature-split tables (experiment build only, -DET_FSPLIT: measured slower, and the
+    // slice loop's registers cost the default kernel 1.6% of the headline when compiled in)
     if constexpr (D == 128 && sizeof(T) == 4) {
         const uint32_t fg = e >> 16;
         if (fg != 0u) {  // a feature slice of a split table (build_stripe_map)
@@ -613,6 +616,7 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
             return;
         }
     }
+#endif
     if constexpr (SG) {
         if ((sm.ntload_mask >> t) & 1u)
             run_bags_s<T, A, U, NT, true, sg_bpl<T>(D)>(pack.d[t], batch, dst, ld_dst, chunk,
@@ -975,6 +979,9 @@ inline void build_stripe_map(const LookupPack& pack, int n, int es, StripeMap& s
     sm.fsplit_g = tu.fsplit_g;
     for (int t = 0; t < n; ++t) {
         bytes[t] = pack.d[t].nrows * pack.d[t].ld_table * es;
+#ifndef ET_FSPLIT
+        can_split = false;  // the slice loop is not compiled in (striped_body)
+#endif
         if (can_split && bytes[t] > tu.light_bytes && bytes[t] <= tu.fsplit_bytes &&
             pack.d[t].cols_per_page == 0 && pack.d[t].dim == 128 &&
             n + (nsp + 1) * (tu.fsplit_g - 1) <= kMaxStripeEntries) {
