@@ -9,6 +9,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "embtab.h"
@@ -61,6 +62,23 @@ inline int elsize(int dtype) {
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Tuning knobs.  The shipped library reads NO environment variable: ET_KNOB(name, dflt) is
+// the tuned default, a compile-time constant.  An experiment build (-DET_EXPERIMENTS,
+// tools/exp_build.sh, never the library the package loads) reads `name` from the
+// environment instead (an integer; unset = dflt), so a sweep needs no source edit.  Every
+// knob selects between correct variants only (schedules, grids, thresholds): results are
+// bit-identical whatever its value.  tests/test_knobs.py checks that the shipped library
+// carries no knob name.
+#ifdef ET_EXPERIMENTS
+inline long long env_knob(const char* name, long long dflt) {
+    const char* e = getenv(name);
+    return e && *e ? atoll(e) : dflt;
+}
+#define ET_KNOB(name, dflt) ((decltype(dflt))::et::env_knob(name, (long long)(dflt)))
+#else
+#define ET_KNOB(name, dflt) (dflt)
+#endif
 
 // ---------------------------------------------------------------------------
 // Device-side helpers

@@ -31,8 +31,11 @@
 
 namespace et {
 
+struct XcdQueue;
 struct LookupPack {
     et_lookup_desc d[ET_MAX_TABLES_PER_LAUNCH];
+    // the caller's queue block (et_maplookup_prealloc_q), or null: the static stripe schedule
+    XcdQueue* queue = nullptr;
 };
 
 // Geometry of the vector path for element type T and feature size D.
@@ -671,33 +674,35 @@ __global__ __launch_bounds__(256) void k_pooled_vec_striped(LookupPack pack, Str
 #endif
 }
 
-// Per-XCD work queues (ET_SCHED=queue): the same stripe map, but a
-// workgroup takes its item from the queue of the XCD it actually runs on (one atomic head
-// per XCD, items in the static schedule's order) and, once that queue is empty, from the
-// other XCDs' queues, so an XCD whose stripes run faster (the static schedule's XCDs
-// finished between 1184 and 1266 us, profiles/r03/b/wg_timeline.json) takes over the
-// tail of the slower ones.  The grid has exactly as many workgroups as items, so every
-// workgroup finds one; the last workgroup to finish resets the heads (atomically) for the
-// next launch on the same stream.  Each stream has a queue block of its own (kQueueSlots
-// per device; launches on one stream never overlap) and a captured launch keeps the static
-// schedule, so a graph replayed on another stream cannot share a block.  Which workgroup
-// sums which bags never changes a result: bit-identical to the static schedule.
-constexpr int kQueueSlots = 64;
+// Per-XCD work queues: the same stripe map, but a workgroup takes its
+// item from the queue of the XCD it actually runs on (one atomic head per XCD, items in the
+// static schedule's order) and, once that queue is empty, from the other XCDs' queues, so an
+// XCD whose stripes run faster (the static schedule's XCDs finished between 1184 and 1266 us,
+// profiles/r03/b/wg_timeline.json) takes over the tail of the slower ones.  The grid has
+// exactly as many workgroups as items, so every workgroup finds one.  The heads live in a
+// queue block the CALLER owns (et_maplookup_prealloc_q, ET_LOOKUP_QUEUE_BYTES, zero before its
+// first use) and the last workgroup to finish resets them, so the block is zero again when
+// the launch completes: stream order makes the block safe for every later launch on the same
+// stream (a HIP graph replay included), and a block is never shared by launches the library
+// could not order (round 4 kept one block per (device, stream handle) in the library —
+// a per-thread default stream, a re-created stream handle or another device's
+// stream could share one).  Which workgroup sums which bags never changes a result:
+// bit-identical to the static schedule.
 struct XcdQueue {
     uint32_t head[kXcds];
     uint32_t done;
-    uint32_t pad[32 - kXcds - 1];  // one 128-byte line per block
+    uint32_t pad[32 - kXcds - 1];  // one 128-byte line
 };
-__device__ XcdQueue g_xcd_queue[kQueueSlots];
+static_assert(sizeof(XcdQueue) == ET_LOOKUP_QUEUE_BYTES, "queue block size (include/embtab.h)");
 
 template <typename T, typename A, int D, int U, bool NT, bool SG>
 __global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, StripeMap sm,
                                                            int ntables, int64_t batch,
                                                            T* __restrict__ dst, int64_t ld_dst,
                                                            int rounds, int64_t stripe_chunks,
-                                                           int64_t nchunks, int qslot) {
+                                                           int64_t nchunks) {
     __shared__ uint32_t s_item;
-    XcdQueue& q = g_xcd_queue[qslot];
+    XcdQueue& q = *pack.queue;
     const uint32_t per = (uint32_t)(ntables * stripe_chunks);  // items per XCD
     if (threadIdx.x == 0) {
         uint32_t xcc;
@@ -717,6 +722,7 @@ __global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, Stri
     const uint32_t it = s_item;
     if (it != ~0u) {
         int64_t slot = (int64_t)(it % per);
+#ifdef ET_EXPERIMENTS
         if (sm.qorder == 1 && sm.nheavy > 0 && sm.nheavy < ntables) {
             // heavy-first: the queue's first nheavy * stripe_chunks items are the heavy
             // tables' chunks, then the light ones (slot = j * ntables + k, as the static order)
@@ -730,6 +736,7 @@ __global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, Stri
             slot = slot < ln ? (slot / nl) * ntables + sm.nheavy + slot % nl
                              : ((slot - ln) / sm.nheavy) * ntables + (slot - ln) % sm.nheavy;
         }
+#endif
         striped_body<T, A, D, U, NT, false, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
                                                 stripe_chunks, nchunks, (int)(it / per), slot);
     }
@@ -739,27 +746,7 @@ __global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, Stri
     }
 }
 
-// The queue block of stream s on the current device, or -1 (capturing, or more than
-// kQueueSlots streams have launched queued lookups on this device).
-inline int xcd_queue_slot(hipStream_t s) {
-    static std::mutex mu;
-    static std::vector<std::pair<int, hipStream_t>> owners;  // slot -> (device, stream)
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return -1;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return -1;
-    std::lock_guard<std::mutex> lk(mu);
-    int mine = 0;
-    for (const auto& o : owners) {
-        if (o.first != dev) continue;
-        if (o.second == s) return mine;
-        ++mine;
-    }
-    if (mine >= kQueueSlots) return -1;
-    owners.emplace_back(dev, s);
-    return mine;
-}
-
+#ifdef ET_EXPERIMENTS
 // The same kernel held to 64 VGPRs (8 waves per SIMD instead of 7): ET_W8=1 experiment.
 template <typename T, typename A, int D, int U, bool NT, bool NTI = false, bool SG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void
@@ -769,6 +756,7 @@ k_pooled_vec_striped_w8(LookupPack pack, StripeMap sm, int ntables, int64_t batc
     striped_body<T, A, D, U, NT, NTI, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
                                           stripe_chunks, nchunks);
 }
+#endif
 
 // Non-reducing gather (bit copy) of RB-byte rows: each group moves U rows at once.
 template <int RB, bool NT>
@@ -907,12 +895,13 @@ inline int rounds_for(int64_t batch, int64_t bags_per_round, int ntables) {
     return rounds;
 }
 
-// Scheduling knobs (read once; for experiments — the defaults are the tuned choice).
+// Scheduling knobs: the defaults are the tuned choice; an experiment build (-DET_EXPERIMENTS)
+// reads them from the environment once (et_common.h, ET_KNOB).  Every setting is bit-identical.
 struct LookupTuning {
     int striped = 1;               // ET_SCHED=linear disables the XCD stripe schedule
-    // per-XCD work queues (k_pooled_vec_queued) by default: headline 1.261-1.262 vs
-    // 1.270-1.271 ms for the static stripe schedule (A/B twice on one box, round 4,
-    // profiles/r04/queue_ab.txt); ET_SCHED=stripe restores the static schedule
+    // per-XCD work queues (k_pooled_vec_queued) wherever the caller passes a queue block:
+    // headline 1.261-1.262 vs 1.270-1.271 ms for the static stripe schedule (A/B twice on one
+    // box, round 4, profiles/r04/queue_ab.txt); ET_SCHED=stripe keeps the static schedule
     int queued = 1;
     // Tables larger than the 256 MiB Infinity Cache cannot stay cache resident: their
     // rows are loaded non-temporally so they do not evict the light tables from L2
@@ -937,26 +926,27 @@ struct LookupTuning {
 inline const LookupTuning& tuning() {
     static LookupTuning t = [] {
         LookupTuning v;
+#ifdef ET_EXPERIMENTS
         if (const char* e = getenv("ET_SCHED")) {
             v.striped = strcmp(e, "linear") != 0;
             v.queued = v.striped && strcmp(e, "stripe") != 0;
         }
-        if (const char* e = getenv("ET_NTLOAD")) v.ntload = atoi(e);
-        if (const char* e = getenv("ET_NTLOAD_BYTES")) v.ntload_bytes = atoll(e);
-        if (const char* e = getenv("ET_NTIDX")) v.ntidx = atoi(e);
-        if (const char* e = getenv("ET_ROUNDS")) v.max_rounds = atoi(e) > 0 ? atoi(e) : 1;
-        if (const char* e = getenv("ET_LIGHT_BYTES")) v.light_bytes = atoll(e);
-        if (const char* e = getenv("ET_U")) v.rows_in_flight = atoi(e);
-        if (const char* e = getenv("ET_W8")) v.w8 = atoi(e);
-        if (const char* e = getenv("ET_SGPR")) v.sgpr = atoi(e);
-        if (const char* e = getenv("ET_SG256")) v.sg256 = atoi(e);
-        if (const char* e = getenv("ET_HEAVY_PRIO")) v.heavy_prio = atoi(e);
-        if (const char* e = getenv("ET_QORDER")) v.qorder = atoi(e);
-        if (const char* e = getenv("ET_FSPLIT_BYTES")) v.fsplit_bytes = atoll(e);
-        if (const char* e = getenv("ET_FSPLIT_G")) {
-            const int g = atoi(e);
-            v.fsplit_g = g == 2 || g == 8 ? g : 4;
-        }
+        v.ntload = (int)ET_KNOB("ET_NTLOAD", v.ntload);
+        v.ntload_bytes = ET_KNOB("ET_NTLOAD_BYTES", v.ntload_bytes);
+        v.ntidx = (int)ET_KNOB("ET_NTIDX", v.ntidx);
+        v.max_rounds = (int)ET_KNOB("ET_ROUNDS", v.max_rounds);
+        if (v.max_rounds < 1) v.max_rounds = 1;
+        v.light_bytes = ET_KNOB("ET_LIGHT_BYTES", v.light_bytes);
+        v.rows_in_flight = (int)ET_KNOB("ET_U", v.rows_in_flight);
+        v.w8 = (int)ET_KNOB("ET_W8", v.w8);
+        v.sgpr = (int)ET_KNOB("ET_SGPR", v.sgpr);
+        v.sg256 = (int)ET_KNOB("ET_SG256", v.sg256);
+        v.heavy_prio = (int)ET_KNOB("ET_HEAVY_PRIO", v.heavy_prio);
+        v.qorder = (int)ET_KNOB("ET_QORDER", v.qorder);
+        v.fsplit_bytes = ET_KNOB("ET_FSPLIT_BYTES", v.fsplit_bytes);
+        const int g = (int)ET_KNOB("ET_FSPLIT_G", 4);
+        v.fsplit_g = g == 2 || g == 8 ? g : 4;
+#endif
         return v;
     }();
     return t;
@@ -1035,6 +1025,7 @@ int launch_pooled_vec(const LookupPack& pack, int n, int64_t batch, void* dst, i
     if constexpr (PG)  // paged tables: one schedule, the default rows in flight
         return launch_pooled_vec_u<T, A, D, VecGeom<T, D>::U, NT, true>(pack, n, batch, dst,
                                                                          ld_dst, s);
+#ifdef ET_EXPERIMENTS
     if constexpr (D == 128 && __is_same(T, float)) {
         switch (tuning().rows_in_flight) {
             case 4: return launch_pooled_vec_u<T, A, D, 4, NT>(pack, n, batch, dst, ld_dst, s);
@@ -1042,6 +1033,7 @@ int launch_pooled_vec(const LookupPack& pack, int n, int64_t batch, void* dst, i
             default: break;
         }
     }
+#endif
     return launch_pooled_vec_u<T, A, D, VecGeom<T, D>::U, NT>(pack, n, batch, dst, ld_dst, s);
 }
 
@@ -1065,24 +1057,24 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         const int64_t stripe_chunks = (nchunks + kXcds - 1) / kXcds;
         const int64_t grid = (int64_t)kXcds * ne * stripe_chunks;
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
-        const int qslot = tuning().queued ? xcd_queue_slot(s) : -1;
-        if (qslot >= 0 && grid < 0xffffffffll) {
+        if (pack.queue && tuning().queued && grid < 0xffffffffll) {
             if constexpr (kSG) {
                 if (sg) {
                     hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, true>),
                                        dim3((unsigned)grid), dim3(256), 0, s, pack, sm, ne, batch,
                                        reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
-                                       nchunks, qslot);
+                                       nchunks);
                     ET_LAUNCH_CHECK("k_pooled_vec_queued");
                     return ET_OK;
                 }
             }
             hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, false>), dim3((unsigned)grid),
                                dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
-                               ld_dst, rounds, stripe_chunks, nchunks, qslot);
+                               ld_dst, rounds, stripe_chunks, nchunks);
             ET_LAUNCH_CHECK("k_pooled_vec_queued");
             return ET_OK;
         }
+#ifdef ET_EXPERIMENTS
         if constexpr (kSG) {
             if (sg && tuning().w8) {
                 hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT, false, true>),
@@ -1092,6 +1084,9 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
                 ET_LAUNCH_CHECK("k_pooled_vec_striped");
                 return ET_OK;
             }
+        }
+#endif
+        if constexpr (kSG) {
             if (sg) {
                 hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT, false, true>),
                                    dim3((unsigned)grid), dim3(256), 0, s, pack, sm, ne, batch,
@@ -1101,6 +1096,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
                 return ET_OK;
             }
         }
+#ifdef ET_EXPERIMENTS
         if (tuning().w8 && D == 128 && __is_same(T, float))
             hipLaunchKernelGGL((k_pooled_vec_striped_w8<T, A, D, U, NT>), dim3((unsigned)grid),
                                dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
@@ -1110,6 +1106,7 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
                                dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
                                ld_dst, rounds, stripe_chunks, nchunks);
         else
+#endif
             hipLaunchKernelGGL((k_pooled_vec_striped<T, A, D, U, NT>), dim3((unsigned)grid),
                                dim3(256), 0, s, pack, sm, ne, batch, reinterpret_cast<T*>(dst),
                                ld_dst, rounds, stripe_chunks, nchunks);
@@ -1292,7 +1289,8 @@ int validate_lookup(const et_lookup_desc* descs, int ntables, int64_t batch, con
 }
 
 int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t batch,
-                    void* dst, int64_t ld_dst, uint32_t flags, hipStream_t s) {
+                    void* dst, int64_t ld_dst, uint32_t flags, hipStream_t s,
+                    void* queue = nullptr) {
     const int es = elsize(dtype);
     if (es == 0) return fail(ET_ERR_UNSUPPORTED, "unknown dtype %d", dtype);
     const int v = validate_lookup(descs, ntables, batch, dst, ld_dst);
@@ -1334,6 +1332,7 @@ int lookup_dispatch(int dtype, const et_lookup_desc* descs, int ntables, int64_t
         if (done[t0] || kind_of[t0] < 0) continue;
         // Collect the group of t0 (same kind, and same dim unless generic).
         LookupPack pack;
+        pack.queue = static_cast<XcdQueue*>(queue);  // launches of one call are stream-ordered
         int n = 0;
         const GroupKind kind = (GroupKind)kind_of[t0];
         const int D = descs[t0].dim;
@@ -1476,6 +1475,16 @@ extern "C" int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int
     // f16 pool == 1 tables are bit copies; the flag only matters for pool >= 2, where the
     // group kind is kPooledVec / kGeneric.
     return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags, s);
+}
+
+extern "C" int et_maplookup_prealloc_q(int dtype, const et_lookup_desc* descs, int32_t ntables,
+                                       int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
+                                       void* queue, void* stream) {
+    et::clear_err();
+    if (queue && (reinterpret_cast<uintptr_t>(queue) & 15u))
+        return et::fail(ET_ERR_ARG, "queue block is not 16-byte aligned");
+    return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags,
+                               static_cast<hipStream_t>(stream), queue);
 }
 
 extern "C" int et_maplookup_prealloc_to(int dtype, int dst_dtype, const et_lookup_desc* descs,

@@ -88,6 +88,7 @@ struct LoopComm {
     LoopGroup* g;
     int rank;
     bool exchange_failed = false;  // the last failure of this rank came from loop_exchange
+    int exchanges_left = 0;        // collectives of the current step not yet joined
 };
 
 // A rank that fails before it joins a collective never arrives: mark the group broken and
@@ -110,6 +111,7 @@ static LoopComm* as_loop(const void* comm) {
 // recv[p] (rbytes[p]) from it.  Collective over the group's ranks; stream-ordered on st.
 static int loop_exchange_impl(LoopComm* c, LoopPost&& mine, hipStream_t st);
 static int loop_exchange(LoopComm* c, LoopPost&& mine, hipStream_t st) {
+    if (c->exchanges_left > 0) --c->exchanges_left;
     const int rc = loop_exchange_impl(c, std::move(mine), st);
     c->exchange_failed = rc != ET_OK;
     return rc;
@@ -622,9 +624,13 @@ static int check_local(Sharded* s, const et_lookup_desc* local, int32_t nlocal) 
 }
 
 // A loopback rank whose step fails outside a collective (argument checks, a lookup launch)
-// aborts its group, so its peers' pending collectives fail fast.
+// BEFORE it has joined every collective of the step aborts its group, so its peers' pending
+// collectives fail fast.  A failure after its last collective (an assembly
+// launch) leaves the group alone: its peers' step completed.
 static int loop_guard(Sharded* s, int rc) {
-    if (rc != ET_OK && s->loop && !s->loop->exchange_failed) et::loop_abort(s->loop);
+    if (rc != ET_OK && s->loop && !s->loop->exchange_failed && s->loop->exchanges_left > 0)
+        et::loop_abort(s->loop);
+    if (s->loop) s->loop->exchanges_left = 0;
     return rc;
 }
 
@@ -640,7 +646,10 @@ extern "C" int et_sharded_maplookup(void* handle, const et_lookup_desc* local, i
     et::clear_err();
     if (!handle) return et::fail(ET_ERR_ARG, "handle is NULL");
     Sharded* s = (Sharded*)handle;
-    if (s->loop) s->loop->exchange_failed = false;
+    if (s->loop) {
+        s->loop->exchange_failed = false;
+        s->loop->exchanges_left = s->exchange == ET_EXCHANGE_ALLTOALL ? 1 : s->chunks;
+    }
     return loop_guard(s, sharded_maplookup(s, local, nlocal, dst, ld_dst, workspace, ws_bytes,
                                            flags, stream));
 }
@@ -651,7 +660,10 @@ extern "C" int et_sharded_piece_grads(void* handle, const void* delta, int64_t l
     et::clear_err();
     if (!handle) return et::fail(ET_ERR_ARG, "handle is NULL");
     Sharded* s = (Sharded*)handle;
-    if (s->loop) s->loop->exchange_failed = false;
+    if (s->loop) {
+        s->loop->exchange_failed = false;
+        s->loop->exchanges_left = 1;
+    }
     return loop_guard(s, sharded_piece_grads(s, delta, ld_delta, recv, workspace, ws_bytes,
                                              stream));
 }

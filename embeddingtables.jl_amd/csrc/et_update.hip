@@ -44,9 +44,7 @@ struct UpdatePack {
 
 // Counters in the workspace.
 enum { kCntU = 0, kCntC = 1, kCntM = 2, kCntT = 3,
-       kCntNext = 5,     // next plain chain item (k_sgd_chains)
-       kCntHfNext = 6,   // next helper-fed chain item
-       kCntHfItems = 7,  // helper-fed items (the first of the chain order)
+       kCntNext = 5,     // next chain item (k_sgd_chains)
        kCntSlots = 16 };
 
 __device__ __forceinline__ int table_of_key(const UpdatePack& p, int ntables, uint32_t key) {
@@ -335,7 +333,13 @@ __device__ __forceinline__ T sgd_apply_t(T w, C acc, C eta_c, double eta64) {
         if constexpr (MODE == 0) return __fma_rn(-eta_c, acc, (double)w);
         return __dsub_rn((double)w, __dmul_rn(eta_c, acc));
     } else if constexpr (MODE == 0) {
-        return (T)__builtin_fmaf(-(float)eta_c, (float)acc, (float)w);
+        // one fp32 fma, THEN one rounding to T.  The barrier keeps the compiler from folding
+        // fptrunc(fma) into v_fma_mixlo_f16, which rounds the exact product-sum to half once
+        // instead of going through fp32: a different result in rare ties (round 5 found 6 of
+        // 64 K Float16 elements off by one ulp against the oracle's fmaf + f32->f16)
+        float r = __builtin_fmaf(-(float)eta_c, (float)acc, (float)w);
+        asm volatile("" : "+v"(r));
+        return (T)r;
     } else if constexpr (__is_same(C, float)) {
         return (T)__fsub_rn((float)w, __fmul_rn(eta_c, acc));
     } else {  // Float16 arithmetic, two roundings (-ffp-contract=off: no fma)
@@ -1111,12 +1115,6 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
 // cost so the longest chains are dispatched first), k_chain_emit (the entries).  Update phase: the chain role of
 // k_sgd_exact, beside the chunk pass (single-chunk columns) and the singles in ONE
 // launch, so the hottest chains (834,828 adds on the config-4 batch) overlap the rest.
-// A positive integer from the environment (experiment knobs), else dflt.
-inline unsigned env_uint(const char* name, unsigned dflt) {
-    const char* e = getenv(name);
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? (unsigned)v : dflt;
-}
 
 constexpr int kChainGroup = kChainAsmTrip;  // entries per trip of the asm loop
 constexpr int kChainPad = kChainAsmPad;     // readable entries past the last trip
@@ -1372,23 +1370,16 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
             continue;
         }
         uint32_t E[5] = {0u, 0u, 0u, 0u, 0u};
-        if (tcnt) {
-            for (uint32_t i = (uint32_t)lane; i < nt; i += 64)
+        for (uint32_t i = (uint32_t)lane; i < nt; i += 64)
 #pragma unroll
-                for (int k = 0; k < 5; ++k) E[k] += tcnt[5 * (t0 + i) + k];
-        } else if (lane == 0) {  // S = 1 only (fed chains): one entry per occurrence
-            const uint32_t u = mlist[m];
-            E[0] = seg_start[u + 1] - seg_start[u];
-        }
+            for (int k = 0; k < 5; ++k) E[k] += tcnt[5 * (t0 + i) + k];
         int best = 0;
         uint64_t bc = ~0ull;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             E[k] = wave_sum_u32(E[k]);
-            // kmax >> 8: a per-entry latency term (doubled slots, ET_LAT_REG) that favours
-            // fewer, longer entries for latency-bound chains; kmax & 255 the largest log2 S
-            const uint64_t c = (uint64_t)E[k] * (chain_entry_cost2(1u << k) + ((uint32_t)kmax >> 8));
-            if (k <= (kmax & 255) && c < bc) bc = c, best = k;  // 0: every entry one occurrence
+            const uint64_t c = (uint64_t)E[k] * chain_entry_cost2(1u << k);
+            if (k <= kmax && c < bc) bc = c, best = k;  // kmax: the largest log2 S
         }
         if (lane == 0) {
             cnt[m] = cdiv_u32(E[best], kChainGroup) * kChainGroup + kChainPad;
@@ -1520,41 +1511,6 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
     }
 }
 
-// Index phase 5 for S = 1 plans (fed chains): every occurrence is one entry (r = 1) of its
-// gradient column, in occurrence order — a copy of the sorted pairs' bags; the column's last
-// tile pads to the planned count (bag = batch: loads +0) and writes the descriptor.
-__global__ __launch_bounds__(256) void k_chain_emit1(UpdatePack pack, int ntables,
-                                                     const uint32_t* __restrict__ keys,
-                                                     const uint32_t* __restrict__ vals,
-                                                     const uint32_t* __restrict__ seg_start,
-                                                     const uint32_t* __restrict__ mlist,
-                                                     const uint32_t* __restrict__ counters,
-                                                     const uint32_t* __restrict__ tile0,
-                                                     const uint32_t* __restrict__ tile_col,
-                                                     const uint32_t* __restrict__ cnt,
-                                                     const uint2* __restrict__ info,
-                                                     const uint32_t* __restrict__ e0s,
-                                                     uint32_t* __restrict__ ent,
-                                                     ChainCol* __restrict__ chains) {
-    const uint32_t M = counters[kCntM], T = counters[kCntT];
-    for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
-        const ChainTile c = chain_tile(pack, ntables, keys, seg_start, mlist, tile0, tile_col, M,
-                                       T, tile);
-        const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
-        const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
-        const uint32_t e0 = e0s[c.m], at = e0 + (c.a - c.ss);
-        for (uint32_t i = threadIdx.x; i < n; i += 256)
-            ent[at + i] = chain_entry(1u, (vals[c.a + i] - occ_off) / pool);
-        if (c.ti + 1 == c.nt) {
-            const uint32_t P = cnt[c.m];
-            const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[c.t].batch);
-            for (uint32_t i = e0 + info[c.m].y + threadIdx.x; i < e0 + P; i += 256) ent[i] = pad;
-            if (threadIdx.x == 0)
-                chains[c.m] = ChainCol{keys[c.ss], e0, (P - kChainPad) / kChainGroup, 1u};
-        }
-    }
-}
-
 // Debug check of the chain plan (ET_CHAIN_CHECK=1): every entry of every chain addresses
 // a gradient column of its table's batch with at most S adds, the entries carrying
 // adds number exactly E and precede the padding; a violation is counted in the device
@@ -1612,7 +1568,6 @@ constexpr int kEcBags = 256;     // bags per workgroup of k_ec_count / k_ec_emit
 constexpr int kEcMaxPool = 255;  // per-bag counts fit a byte
 constexpr int kEcMaxBatch = 1 << 20;
 constexpr int kEcStats = 8;      // per (column, block): occurrences, entries at S = 1..16
-constexpr uint32_t kHfMinOcc = 65536;  // helper-fed chains: at least this many occurrences
 
 // Early HOT columns of the larger tables (round 4, ET_EH): every table of more than
 // kEcMaxRows rows gets kEhK "slots" — the columns a sample of its first kEhSampleBags bags
@@ -1649,14 +1604,8 @@ inline bool eh_table(const et_update_desc& d) {
 }
 
 // On by default: config-4 exact update 4.05-4.06 ms with, 4.24-4.25 without (the exact
-// grid cap on, A/B twice on one box, profiles/r04/ab_exact_grid.txt); ET_EH=0 turns it off.
-inline bool eh_enabled() {
-    static const bool v = [] {
-        const char* e = getenv("ET_EH");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
+// grid cap on, A/B twice on one box, profiles/r04/ab_exact_grid.txt).
+inline bool eh_enabled() { return ET_KNOB("ET_EH", 1) != 0; }
 
 // One workgroup per EH entry: count the sampled bags' columns in an LDS hash table, keep the
 // columns expected to reach kEhMinOcc occurrences, at most kEhK of them (the most frequent;
@@ -1847,8 +1796,8 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
     uint64_t bc = ~0ull;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        const uint64_t cc = (uint64_t)v[1 + k] * (chain_entry_cost2(1u << k) + ((uint32_t)kmax >> 8));
-        if (k <= (kmax & 255) && cc < bc) bc = cc, best = k;  // as k_chain_choose
+        const uint64_t cc = (uint64_t)v[1 + k] * chain_entry_cost2(1u << k);
+        if (k <= kmax && cc < bc) bc = cc, best = k;  // as k_chain_choose
     }
     const bool is_chain = v[0] > chunk;  // wave-uniform
     const uint32_t S = is_chain ? (1u << best) : 0u, E = is_chain ? v[1 + best] : 0u;
@@ -1880,26 +1829,23 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
 // EC step 3 (one workgroup): the cost order of the EC columns (as k_chain_plan) and their
 // count (counters[kCntM], read by the chain role).
 __global__ __launch_bounds__(1024) void k_ec_order(EcList ec, const uint2* __restrict__ info,
-                                                   const uint32_t* __restrict__ nocc, int ns,
+                                                   int ns,
                                                    uint32_t* __restrict__ order,
                                                    uint32_t* __restrict__ counters) {
-    __shared__ uint32_t hist[66];
+    __shared__ uint32_t hist[65];
     const uint32_t M = ec.col0[ec.n];
-    if (threadIdx.x < 66) hist[threadIdx.x] = 0u;
+    if (threadIdx.x < 65) hist[threadIdx.x] = 0u;
     __syncthreads();
-    // bucket 0: the helper-fed columns (long runs, many occurrences); then by log2 cost
-    auto bucket = [&](uint32_t g) {
+    auto bucket = [&](uint32_t g) {  // leading zeros of the cost: 0 = costliest, 64 = none
         const uint2 in = info[g];
-        if (in.x >= 8u && nocc[g] >= kHfMinOcc) return 0u;
         const uint64_t cc = (uint64_t)in.y * chain_entry_cost2(in.x);
-        return cc ? 1u + (uint32_t)__clzll((long long)cc) : 65u;
+        return cc ? (uint32_t)__clzll((long long)cc) : 64u;
     };
     for (uint32_t g = threadIdx.x; g < M; g += 1024) atomicAdd(&hist[bucket(g)], 1u);
     __syncthreads();
     if (threadIdx.x == 0) {
-        counters[kCntHfItems] = hist[0] * (uint32_t)ns;
         uint32_t run = 0;
-        for (int k = 0; k < 66; ++k) {
+        for (int k = 0; k < 65; ++k) {
             const uint32_t h = hist[k];
             hist[k] = run;
             run += h;
@@ -2029,323 +1975,153 @@ __device__ __forceinline__ float chain_walk_quad(const uint32_t* ent, uint32_t n
     return acc;
 }
 
+// Whether a chain of a table with this gradient can take the hand-scheduled Float32 loops
+// (et_chain_asm.h, chain_walk_quad): their gradient addresses are 32-bit byte offsets in one
+// range-checked buffer — bag * ld * 4 + 4 * feature from 24-bit factors, and a padding entry
+// (bag = batch) must land past the range to load +0 — so (batch + 1) * ld * 4 stays below
+// 2^32 and ld below 2^22.  Any other chain takes chain_walk_wide (64-bit addresses).
+__host__ __device__ inline bool chain_asm_ok(int64_t batch, int64_t ld) {
+    return ld < (1ll << 22) && (uint64_t)(batch + 1) * (uint64_t)ld * 4u < (1ull << 32);
+}
+
+// The serial sum of one chain over one 64-feature slice (lane = feature), with 64-bit
+// gradient addresses and any element type: the reference's loop (src/sparseupdate.jl:110-127,
+// acc += delta[:, bag] once per occurrence, in the accumulator type) taken entry by entry —
+// r adds of the entry's gradient column.  The Float32 chains whose gradient the asm loop's
+// 32-bit offsets cannot reach (chain_asm_ok) and the Float64 / Float16 / BFloat16 chains
+// take it.  Entries are wave-uniform (scalar loads); the gradient loads run kWideAhead
+// entries ahead, each from a wave-uniform row address (a padding entry, r = 0, loads row 0
+// of the gradient and adds nothing).  ent: ngr x 64 entries, then >= kChainPad padding.
+constexpr int kWideAhead = 16;
+
+template <typename T>
+__device__ __forceinline__ T wide_load(const T* delta, uint64_t ld, uint32_t fc, uint32_t e) {
+    const uint64_t bag = (e >> 24) ? (uint64_t)(e & 0xffffffu) : 0u;
+    return delta[bag * ld + fc];
+}
+
+template <typename T, typename C>
+__device__ __forceinline__ C chain_walk_wide(const uint32_t* ent, uint32_t ngr, const T* delta,
+                                             uint64_t ld, uint32_t fc, C acc) {
+    static_assert(kChainGroup % kWideAhead == 0 && kChainPad >= kWideAhead, "wide walk layout");
+    uint32_t en[kWideAhead];
+    T x[kWideAhead];
+#pragma unroll
+    for (int k = 0; k < kWideAhead; ++k) {
+        en[k] = ent[k];
+        x[k] = wide_load(delta, ld, fc, en[k]);
+    }
+    const uint32_t ne = ngr * (uint32_t)kChainGroup;
+    for (uint32_t h = 0; h < ne; h += kWideAhead) {
+#pragma unroll
+        for (int k = 0; k < kWideAhead; ++k) {
+            const uint32_t r = en[k] >> 24;
+            const C v = C(x[k]);
+            en[k] = ent[h + kWideAhead + k];  // inside the padding past the last trip
+            x[k] = wide_load(delta, ld, fc, en[k]);
+            for (uint32_t j = 0; j < r; ++j) acc = acc + v;
+        }
+    }
+    return acc;
+}
+
 // Update phase, chain role: one (column, 64-feature slice, quarter) item of the cost-
-// ordered list: the serial sum of the slice's gradient columns and the update.  An S = 1
-// chain takes its four quarters as four items (the quad walk, 16 features each); any other
-// chain takes the whole slice in quarter 0 (the other quarters return at once).
-template <int MODE, bool NT>
+// ordered list: the serial sum of the slice's gradient columns and the update.  A Float32
+// S = 1 chain of at least quad_min 64-entry groups takes its four quarters as four items
+// (the quad walk, 16 features each); any other chain takes the whole slice in quarter 0
+// (the other quarters return at once).  T is the table and gradient type, C the
+// accumulator (sgd_apply_t).
+template <typename T, typename C, int MODE, bool NT>
 __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntables,
                                                const ChainCol* __restrict__ chains,
                                                const uint32_t* __restrict__ order,
                                                const uint32_t* __restrict__ ent, int ns,
-                                               float eta32, double eta64, uint32_t it4,
-                                               int how) {
+                                               C eta_c, double eta64, uint32_t it4,
+                                               uint32_t quad_min) {
+    constexpr bool kF32 = __is_same(T, float);
     const int lane = threadIdx.x & 63;
-    const bool plain = (how & 1) != 0;  // debug: the plain C++ loop for every chain
     const uint32_t quarter = it4 % (uint32_t)kQuadItems, it = it4 / (uint32_t)kQuadItems;
     const ChainCol c = chains[order[it / (uint32_t)ns]];
     if (c.S == 0u) return;
-    // the quad walk for long S = 1 chains only (how >> 4 = the minimum in 64-entry groups):
-    // it spends 4 waves where the 64-feature loop spends one, so short chains, which are
-    // throughput- rather than latency-bound, keep the loop; how & 2 turns it off
-    const bool quad = c.S == 1u && (how & 3) == 0 && c.ngr >= ((uint32_t)how >> 4);
-    if (!quad && quarter != 0u) return;
     const int t = table_of_key(pack, ntables, c.key);
     const et_update_desc& d = pack.d[t];
-    if (quad) {
-        const int f0 = (int)(it % (uint32_t)ns) * 64 + (int)quarter * 16;
-        if (f0 >= d.dim) return;  // uniform
-        const int f = f0 + (lane & 15);
-        const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
-        const uint32_t ld = (uint32_t)d.ld_delta;
-        const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
-        const float* delta = reinterpret_cast<const float*>(
-            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
-            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
-        const uint64_t eb = reinterpret_cast<uint64_t>(ent + c.e0);
-        const uint32_t* e = reinterpret_cast<const uint32_t*>(
-            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)eb) |
-            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(eb >> 32)) << 32);
-        // how & 8: timing experiment only (ET_CHAIN_FAKE=1, wrong results): every entry
-        // loads gradient row 0 (cache-resident), so the walk runs without HBM latency
-        const float acc = chain_walk_quad(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
-                                          (uint32_t)d.batch * ld * 4u, 4u * fc,
-                                          how & 8 ? 0u : 4u * ld);
-        if (lane < 16 && f < d.dim) {
-            float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
-            store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
-        }
-        return;
-    }
-    const int f = (int)(it % (uint32_t)ns) * 64 + lane;
-    if ((int)(it % (uint32_t)ns) * 64 >= d.dim) return;  // uniform
-    const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
-    const uint32_t ld = (uint32_t)d.ld_delta;
-    // the gradient base as a wave-uniform (SGPR) pointer
+    const bool fast = kF32 && chain_asm_ok(d.batch, d.ld_delta);
+    // the quad walk spends 4 waves where the 64-feature loop spends one, so short chains,
+    // which are throughput- rather than latency-bound, keep the loop
+    const bool quad = fast && c.S == 1u && c.ngr >= quad_min;
+    if (!quad && quarter != 0u) return;
+    const int slice = (int)(it % (uint32_t)ns);
+    // the gradient base and the entries as wave-uniform (SGPR) pointers
     const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
-    const float* delta = reinterpret_cast<const float*>(
+    const T* delta = reinterpret_cast<const T*>(
         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
-    const uint32_t* e = ent + c.e0;
-    float acc = 0.0f;
-    if (plain) {  // debug reference of the asm loop: the same adds, plainly
-        const uint32_t ne = c.ngr * kChainGroup;
-        for (uint32_t h = 0; h < ne; ++h) {
-            const uint32_t en = e[h];
-            if ((en >> 24) == 0u) continue;  // padding
-            const float x = delta[(uint64_t)(en & 0xffffffu) * ld + fc];
-            for (uint32_t k = 0; k < (en >> 24); ++k) acc = acc + x;
-        }
-    } else {
-        // range batch * ld * 4 bytes: a padding entry (bag = batch) loads +0
-        const i32x4 rs = chain_rsrc(delta, (uint32_t)d.batch * ld * 4u);
-        const uint32_t ld4 = how & 8 ? 0u : 4u * ld;  // ET_CHAIN_FAKE (timing only)
-        switch (c.S) {
-            case 1: acc = chain_walk_asm<1>(e, c.ngr, rs, 4u * fc, ld4, 0.0f); break;
-            case 2: acc = chain_walk_asm<2>(e, c.ngr, rs, 4u * fc, ld4, 0.0f); break;
-            case 4: acc = chain_walk_asm<4>(e, c.ngr, rs, 4u * fc, ld4, 0.0f); break;
-            case 8:
-                acc = how & 4 ? chain_walk_ring<8>(e, c.ngr, rs, 4u * fc, ld4, 0.0f)
-                              : chain_walk_asm<8>(e, c.ngr, rs, 4u * fc, ld4, 0.0f);
-                break;
-            default:
-                acc = how & 4 ? chain_walk_ring<16>(e, c.ngr, rs, 4u * fc, ld4, 0.0f)
-                              : chain_walk_asm<16>(e, c.ngr, rs, 4u * fc, ld4, 0.0f);
-                break;
-        }
-    }
-    if (f < d.dim) {
-        float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
-        store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
-    }
-}
-
-// The chains of an update phase (early or regular), in their own launch on a side stream:
-// each wave takes the next item of the cost-ordered list from counters[kCntNext] (so the
-// longest chains start first and a late workgroup takes whatever is left), until the list
-// is exhausted.  A chain issues a dependent VALU op about every 4.4 cycles, i.e. it alone
-// nearly fills its SIMD's VALU, so two chains must not share a SIMD: the launch reserves
-// more than half of a CU's LDS (dynamic, untouched), so no other chain workgroup — of this
-// launch or the other chain launch — lands on the same CU, and the workgroup's 4 waves take
-// its 4 SIMDs.  Top priority: the co-resident chunk-pass / singles / index-phase waves
-// (memory bound) take the leftover issue slots.
-constexpr uint32_t kChainReserveLds = 84 * 1024;  // > 80 KiB: one chain workgroup per CU
-
-// ET_CHAIN_FED: chains planned at S = 1 and walked by k_sgd_chains_fed (below), a bit mask
-// of chain lists — 1: the early chains, 2: the regular chains, 4: the early hot columns.
-enum { kFedEarly = 1, kFedRegular = 2, kFedHot = 4 };
-inline int chain_fed_mask() {
-    static const int v = [] {
-        const char* e = getenv("ET_CHAIN_FED");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-inline bool chain_fed(int list) { return (chain_fed_mask() & list) != 0; }
-
-// Helper-fed chains ("HF": the longest early chains, whose runs are long — S >= 8 — and
-// whose columns have at least kHfMinOcc occurrences).  The plain loop spends, per entry of
-// r <= S adds, S masked fmacs and ~6 slots of address, load and mask work in the chain's
-// own wave.  Here a pair of waves shares one item: the helper wave loads each entry's
-// gradient column (lane = feature) and writes it r times into a transposed LDS ring (row
-// = feature, one slot per OCCURRENCE); the consumer wave reads 4 occurrences of its
-// feature per ds_read_b128 and adds them — exactly the reference's serial sum, one add per
-// occurrence, no masks.  The helper writes 16 copies from the entry's first slot (8
-// ds_write2): copies past r are overwritten by the next entry's (the helper writes in
-// order), and ring wrap-around gets a second write; slots are published to the consumer
-// only once valid (`produced`), and a slot is rewritten only once consumed (`consumed`).
-constexpr uint32_t kHfRing = 128;               // logical slots (power of two)
-constexpr uint32_t kHfRow = kHfRing + 32 + 4;   // 16 slack slots each side + bank pad
-constexpr uint32_t kHfK = 16;                   // entries per helper batch (2 in flight)
-constexpr uint32_t kHfWg = 24;                  // HF workgroups (2 pairs each) per launch
-
-struct HfCtl {
-    uint32_t seq, item, produced, consumed;
-};
-
-template <int MODE, bool NT>
-__device__ void hf_pair(const UpdatePack& pack, int ntables, uint32_t* __restrict__ counters,
-                        const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-                        const uint2* __restrict__ info, const uint32_t* __restrict__ nocc,
-                        const uint32_t* __restrict__ ent, int ns, float eta32, double eta64,
-                        float* __restrict__ ring, volatile HfCtl* ctl, bool consumer) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t items = counters[kCntHfItems];
-    float* row = ring + lane * kHfRow + 16;  // this lane's feature row, logical slot 0
-    uint32_t seen = 0;
-    for (;;) {
-        uint32_t it;
-        if (consumer) {
-            it = 0;
-            if (lane == 0) it = atomicAdd(&counters[kCntHfNext], 1u);
-            it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
-            if (lane == 0) {
-                ctl->produced = 0u;
-                ctl->consumed = 0u;
-                ctl->item = it;
-                ctl->seq = seen + 1u;  // in order after the fields (one wave's LDS writes)
-            }
-            ++seen;
-        } else {
-            while (ctl->seq == seen) __builtin_amdgcn_s_sleep(1);
-            ++seen;
-            it = (uint32_t)__builtin_amdgcn_readfirstlane((int)ctl->item);
-        }
-        if (it >= items) return;
-        const uint32_t g = order[it / (uint32_t)ns];
-        const ChainCol c = chains[g];
-        const int t = table_of_key(pack, ntables, c.key);
-        const et_update_desc& d = pack.d[t];
-        const int slice = (int)(it % (uint32_t)ns);
-        if (c.S == 0u || slice * 64 >= d.dim) continue;  // both waves skip the item
-        const int f = slice * 64 + lane;
-        const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
-        const uint32_t n = nocc[g];
-        if (consumer) {
-            float acc = 0.0f;
-            uint32_t q = 0, avail = 0;
-            while (q < n) {
-                if (avail < q + 32u && avail < n) {
-                    avail = ctl->produced;
-                    if (avail < q + 32u && avail < n) {
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                }
-                if (q + 32u <= avail) {  // 32 occurrences: 8 ds_read_b128, in order
-                    const float4* src = reinterpret_cast<const float4*>(row + (q & (kHfRing - 1)));
-                    float4 v[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) v[k] = src[k];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        acc = acc + v[k].x;
-                        acc = acc + v[k].y;
-                        acc = acc + v[k].z;
-                        acc = acc + v[k].w;
-                    }
-                    q += 32u;
-                    ctl->consumed = q;  // every lane writes the same value
-                } else {  // the tail (avail == n)
-                    for (; q < n; ++q) acc = acc + row[q & (kHfRing - 1)];
-                }
-            }
-            if (f < d.dim) {
+    const uint64_t eb = reinterpret_cast<uint64_t>(ent + c.e0);
+    const uint32_t* e = reinterpret_cast<const uint32_t*>(
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)eb) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(eb >> 32)) << 32);
+    if constexpr (kF32) {
+        if (quad) {
+            const int f0 = slice * 64 + (int)quarter * 16;
+            if (f0 >= d.dim) return;  // uniform
+            const int f = f0 + (lane & 15);
+            const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
+            const uint32_t ld = (uint32_t)d.ld_delta;
+            const float acc = chain_walk_quad(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
+                                              (uint32_t)d.batch * ld * 4u, 4u * fc, 4u * ld);
+            if (lane < 16 && f < d.dim) {
                 float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
                                           c.key - pack.row_off[t]) + f;
-                store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
+                store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta_c, eta64));
             }
-        } else {
-            const uint32_t E = info[g].y;  // real entries (padding follows)
-            const uint32_t* e = ent + c.e0;
-            const float* dcol = reinterpret_cast<const float*>(d.delta) + fc;
-            const uint64_t ld = (uint64_t)d.ld_delta;
-            uint32_t p = 0, cons = 0;
-            float x[2][kHfK];
-            uint32_t en[2][kHfK];
-            auto load = [&](int buf, uint32_t j0) {
-#pragma unroll
-                for (uint32_t k = 0; k < kHfK; ++k) {
-                    const uint32_t j = j0 + k;
-                    const uint32_t v = j < E ? e[j] : 0u;
-                    en[buf][k] = v;
-                    x[buf][k] = (v >> 24) ? dcol[(uint64_t)(v & 0xffffffu) * ld] : 0.0f;
-                }
-            };
-            load(0, 0u);
-            for (uint32_t j0 = 0; j0 < E; j0 += 2u * kHfK) {
-#pragma unroll
-                for (int half = 0; half < 2; ++half) {
-                    const uint32_t jb = j0 + (uint32_t)half * kHfK;
-                    if (jb >= E) break;
-                    load(half ^ 1, jb + kHfK);  // the next batch in flight
-#pragma unroll
-                    for (uint32_t k = 0; k < kHfK; ++k) {
-                        const uint32_t r = en[half][k] >> 24;
-                        if (r == 0u) continue;  // past E
-                        // the 16 slots from p may hold the previous lap's occurrences
-                        // [p + 16 - ring, ...): wait until they are consumed
-                        while (cons + kHfRing < p + 16u) {
-                            cons = ctl->consumed;
-                            if (cons + kHfRing < p + 16u) __builtin_amdgcn_s_sleep(1);
-                        }
-                        const uint32_t o = p & (kHfRing - 1);
-                        float* dst = row + o;
-                        const float v = x[half][k];
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) dst[i] = v;
-                        if (o + r > kHfRing) {  // wrapped copies
-                            float* dst2 = dst - kHfRing;
-#pragma unroll
-                            for (int i = 0; i < 16; ++i) dst2[i] = v;
-                        }
-                        p += r;
-                        // LDS requests of a wave are performed in order: the copies land
-                        // before the consumer can read this `produced`
-                        ctl->produced = p;
-                    }
-                }
-            }
+            return;
         }
+    }
+    const int f = slice * 64 + lane;
+    if (slice * 64 >= d.dim) return;  // uniform
+    const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
+    C acc = C(0);
+    bool done = false;
+    if constexpr (kF32) {
+        if (fast) {
+            // range batch * ld * 4 bytes: a padding entry (bag = batch) loads +0
+            const uint32_t ld = (uint32_t)d.ld_delta;
+            const i32x4 rs = chain_rsrc(delta, (uint32_t)d.batch * ld * 4u);
+            switch (c.S) {
+                case 1: acc = chain_walk_asm<1>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+                case 2: acc = chain_walk_asm<2>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+                case 4: acc = chain_walk_asm<4>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+                case 8: acc = chain_walk_asm<8>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+                default: acc = chain_walk_asm<16>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
+            }
+            done = true;
+        }
+    }
+    if (!done) acc = chain_walk_wide<T, C>(e, c.ngr, delta, (uint64_t)d.ld_delta, fc, acc);
+    if (f < d.dim) {
+        T* w = col_ptr<T>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
+        store_scalar<NT>(w, sgd_apply_t<T, C, MODE>(*w, acc, eta_c, eta64));
     }
 }
 
-// The chains of an update phase (early or regular), in their own launch on a side stream.
-// Workgroups [0, nhf) run helper-fed pairs (waves 0/1 and 2/3, one item each at a time,
-// from counters[kCntHfNext]); the others take plain items — each wave the next of the
-// cost-ordered list from counters[kCntNext], which starts past the helper-fed ones — so
-// the longest chains start first and a late workgroup takes whatever is left.  A chain
-// issues a dependent VALU op about every 4.4 cycles, i.e. it alone nearly fills its SIMD's
-// VALU, so two chains must not share a SIMD: the launch reserves more than half of a CU's
-// LDS (the HF rings; untouched by plain workgroups), so no other chain workgroup — of this
-// launch or the other chain launch — lands on the same CU, and the workgroup's 4 waves
-// take its 4 SIMDs.  Top priority: the co-resident chunk-pass / singles / index-phase
-// waves (memory bound) take the leftover issue slots.
-template <int MODE, bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chains(
-    UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
-    const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint2* __restrict__ info, const uint32_t* __restrict__ nocc,
-    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64, int plain,
-    uint32_t nhf) {
-    extern __shared__ float lds[];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    __builtin_amdgcn_s_setprio(3);
-    if (blockIdx.x < nhf) {
-        HfCtl* ctl = reinterpret_cast<HfCtl*>(lds + 2 * 64 * kHfRow);
-        if (threadIdx.x < 2) ctl[threadIdx.x] = HfCtl{0u, 0u, 0u, 0u};
-        __syncthreads();
-        const int pair = wave >> 1;
-        hf_pair<MODE, NT>(pack, ntables, counters, chains, order, info, nocc, ent, ns, eta32,
-                          eta64, lds + pair * 64 * kHfRow, ctl + pair, (wave & 1) == 0);
-    } else {
-        const uint32_t items = counters[kCntM] * (uint32_t)ns * (uint32_t)kQuadItems;
-        for (;;) {
-            uint32_t it = 0;
-            if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
-            it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
-            if (it >= items) break;
-            sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it,
-                                     plain);
-        }
-    }
-    __builtin_amdgcn_s_setprio(0);
-}
+// The chains of an update phase (early, early hot or regular), in their own launch on a side
+// stream: each wave takes the next item of the cost-ordered list from counters[kCntNext] (so
+// the longest chains start first and a late workgroup takes whatever is left), until the
+// list is exhausted.  A chain issues a dependent VALU op about every 4.4 cycles, i.e. it alone
+// nearly fills its SIMD's VALU, so two chains must not share a SIMD: the launch reserves more
+// than half of a CU's LDS (dynamic, untouched), so no other chain workgroup — of this launch
+// or another chain launch — lands on the same CU, and the workgroup's 4 waves take its 4
+// SIMDs.  Top priority: the co-resident chunk-pass / singles / index-phase waves (memory
+// bound) take the leftover issue slots.
+constexpr uint32_t kChainReserveLds = 84 * 1024;  // > 80 KiB: one chain workgroup per CU
 
-// The same chain loop (plain items only) on SIMDs of its own: the kernel writes a255, so
-// it is allocated the whole accumulation-register file besides its VGPRs and no other
-// wave — of the chunk pass, the singles, the index phase — can be resident on its SIMDs
-// while it runs; the chain waves then issue at the SIMD's own rate instead of sharing it
-// (ET_CHAIN_EXCL: bit 0 the early chains, bit 1 the regular ones).
-template <int MODE, bool NT>
-__global__ __launch_bounds__(256) void k_sgd_chains_x(
-    UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
-    const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint2* __restrict__ info, const uint32_t* __restrict__ nocc,
-    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64, int plain,
-    uint32_t nhf) {
-    asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+template <typename T, typename C, int MODE, bool NT>
+__device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
+                                            uint32_t* __restrict__ counters,
+                                            const ChainCol* __restrict__ chains,
+                                            const uint32_t* __restrict__ order,
+                                            const uint32_t* __restrict__ ent, int ns, C eta_c,
+                                            double eta64, uint32_t quad_min) {
     const int lane = threadIdx.x & 63;
     __builtin_amdgcn_s_setprio(3);
     const uint32_t items = counters[kCntM] * (uint32_t)ns * (uint32_t)kQuadItems;
@@ -2354,127 +2130,34 @@ __global__ __launch_bounds__(256) void k_sgd_chains_x(
         if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
         it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
         if (it >= items) break;
-        sgd_chain_item<MODE, NT>(pack, ntables, chains, order, ent, ns, eta32, eta64, it, plain);
+        sgd_chain_item<T, C, MODE, NT>(pack, ntables, chains, order, ent, ns, eta_c, eta64, it,
+                                       quad_min);
     }
     __builtin_amdgcn_s_setprio(0);
 }
 
-// ---- Fed chains (round 4, ET_CHAIN_FED): every chain planned at S = 1 — its entry list
-// is the column's occurrence list, one gradient column (bag) per occurrence, in order, padded
-// to whole 64-entry chunks with bag = batch (loads +0) — and walked by a workgroup of eight
-// waves: wave 0 sums, waves 1-7 gather.  Gatherer p takes chunks p, p + 7, ...: per
-// occurrence one dword load of the 64-feature row (lane = feature; the bag comes from the
-// chunk's entry vector by v_readlane, the row offset as the scalar offset), issued in halves
-// of 32 occurrences so ~64 loads stay in flight per gatherer (7 x 64 occurrences in all);
-// every 4 occurrences of a feature go to LDS as one ds_write_b128 into that feature's row of
-// an LDS ring of kFedSlots occurrence slots (row = feature, slot = occurrence; pitch 516
-// dwords = 4 mod 64 banks, so both the writes and the summing wave's b128 reads are free of
-// bank conflicts — the first version's per-occurrence b32 writes of 16-byte load slices
-// were 8-way conflicted and bounded the walk at ~16 LDS cycles per occurrence).  A gatherer
-// publishes a chunk in its FULL word; the summing wave reads four slots of its feature per
-// ds_read_b128 and adds them in order — exactly the reference's serial sum
-// (src/sparseupdate.jl:110-127), one add per occurrence and no masked slots — and publishes
-// the slots it has consumed (FREE) so gatherers can reuse them.
-constexpr int kFedSlots = 512;              // ring slots (8 chunks of 64 occurrences)
-constexpr int kFedPitch = kFedSlots + 4;    // dwords per feature row: 516 = 4 mod 64
-constexpr int kFedGather = 7;               // gatherer waves per workgroup
-constexpr uint32_t kFedLds = 64u * kFedPitch * 4u;  // the ring rows (132 KB; the control
-                                                    // words are a static LDS array)
-enum { kFedFree = kFedGather, kFedItem = kFedGather + 1, kFedCtl = kFedGather + 2 };
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// The control words live in a static LDS array and are read and written with workgroup-
-// scope relaxed atomics, so they compile to ds_read / ds_write (a volatile generic pointer
-// becomes flat_load / flat_store, whose vmcnt waits would drain the gatherers' loads).
-__device__ __forceinline__ uint32_t fed_get(uint32_t* ctl, int i) {
-    return __hip_atomic_load(ctl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void fed_set(uint32_t* ctl, int i, uint32_t v) {
-    __hip_atomic_store(ctl + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int MODE, bool NT>
-__global__ __launch_bounds__(64 * (kFedGather + 1)) void k_sgd_chains_fed(
+template <typename T, typename C, int MODE, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chains(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, float eta32, double eta64) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ uint32_t ctl[kFedCtl];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t items = counters[kCntM] * (uint32_t)ns;
-    __builtin_amdgcn_s_setprio(3);
-    for (;;) {
-        if (threadIdx.x == 0) {
-            for (int k = 0; k < kFedGather + 1; ++k) fed_set(ctl, k, 0u);
-            fed_set(ctl, kFedItem, atomicAdd(&counters[kCntNext], 1u));
-        }
-        __syncthreads();
-        const uint32_t it = (uint32_t)__builtin_amdgcn_readfirstlane((int)fed_get(ctl, kFedItem));
-        if (it >= items) break;  // workgroup-uniform
-        const ChainCol c = chains[order[it / (uint32_t)ns]];
-        const int slice = (int)(it % (uint32_t)ns);
-        const int t = table_of_key(pack, ntables, c.key);
-        const et_update_desc& d = pack.d[t];
-        const uint32_t nch = c.ngr;
-        float* row = lds + lane * kFedPitch;
-        if (c.S != 0u && slice * 64 < d.dim && nch > 0u) {  // workgroup-uniform
-            if (wave == 0) {  // the serial sum
-                float acc = 0.0f;
-                for (uint32_t ch = 0; ch < nch; ++ch) {
-                    const uint32_t need = ch / (uint32_t)kFedGather + 1u;
-                    while (fed_get(ctl, (int)(ch % (uint32_t)kFedGather)) < need)
-                        __builtin_amdgcn_s_sleep(0);
-                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    const f32x4* src = reinterpret_cast<const f32x4*>(
-                        row + (int)(ch % (uint32_t)(kFedSlots / 64)) * 64);
-                    f32x4 v[16];
-#pragma unroll
-                    for (int m = 0; m < 16; ++m) v[m] = src[m];
-#pragma unroll
-                    for (int m = 0; m < 16; ++m) {
-                        acc = acc + v[m].x;
-                        acc = acc + v[m].y;
-                        acc = acc + v[m].z;
-                        acc = acc + v[m].w;
-                    }
-                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-                    if (lane == 0) fed_set(ctl, kFedFree, (ch + 1u) * 64u);
-                }
-                const int f = slice * 64 + lane;
-                if (f < d.dim) {
-                    float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
-                                              c.key - pack.row_off[t]) + f;
-                    store_scalar<NT>(w, sgd_apply<MODE>(*w, acc, eta32, eta64));
-                }
-            } else {  // gatherer p: chunks p, p + 7, ... (et_chain_asm.h, fed_gather_asm)
-                static_assert(kFedAsmGatherers == kFedGather && kFedFree == kFedGather &&
-                                  kFedSlots == 512, "fed gatherer layout (tools/gen_chain_asm.py)");
-                const uint32_t p = (uint32_t)(wave - 1);
-                const uint32_t ld = (uint32_t)d.ld_delta;
-                const uint32_t nm =
-                    p < nch ? (nch - p + (uint32_t)kFedGather - 1u) / (uint32_t)kFedGather : 0u;
-                if (nm > 0u) {
-                    const uint64_t db = reinterpret_cast<uint64_t>(d.delta);
-                    const float* delta = reinterpret_cast<const float*>(
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
-                    const uint64_t eb = reinterpret_cast<uint64_t>(ent + c.e0);
-                    const float* ep = reinterpret_cast<const float*>(
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)eb) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(eb >> 32)) << 32);
-                    const i32x4 rx = chain_rsrc(delta, (uint32_t)d.batch * ld * 4u);
-                    const i32x4 re = chain_rsrc(ep, nch * 256u);
-                    const uint32_t rowa = (uint32_t)reinterpret_cast<uintptr_t>(row);
-                    const uint32_t ctla = (uint32_t)reinterpret_cast<uintptr_t>(&ctl[0]);
-                    fed_gather_asm(nm, p, re, rx, 4u * (uint32_t)(slice * 64 + lane),
-                                   4u * (uint32_t)lane, 4u * ld, rowa, ctla, ctla + 4u * p);
-                }
-            }
-        }
-        __syncthreads();  // the ring and the control words are free for the next item
-    }
-    __builtin_amdgcn_s_setprio(0);
+    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min) {
+    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
+                                quad_min);
+}
+
+// The same chain loop on SIMDs of its own: the kernel writes a255, so it is allocated the
+// whole accumulation-register file besides its VGPRs and no other wave — of the chunk pass,
+// the singles, the index phase — can be resident on its SIMDs while it runs; the chain waves
+// then issue at the SIMD's own rate instead of sharing it (the early chains and the early hot
+// columns by default, kChainExcl).
+template <typename T, typename C, int MODE, bool NT>
+__global__ __launch_bounds__(256) void k_sgd_chains_x(
+    UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
+    const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min) {
+    asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
+    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
+                                quad_min);
 }
 
 // The rest of the update phase of an exact Float32 call in one launch: blocks [0, nch)
@@ -2727,15 +2410,8 @@ inline Grouped grouped_pairs(const UpdatePack& pack, int ntables, const UpdateWs
 // over the single-chunk columns (k_sgd_exact) — the plan is off the update's critical path.
 inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uint32_t sent,
                              uint32_t chunk, UpdateWs& w, const Grouped& out, hipStream_t s,
-                             uint32_t ec_mask, const EhMap& eh, hipEvent_t cand_ready,
-                             hipEvent_t gate = nullptr, int gate_at = 0) {
+                             uint32_t ec_mask, const EhMap& eh, hipEvent_t cand_ready) {
     if (eh.mask) ET_HIP_CHECK(hipStreamWaitEvent(s, cand_ready, 0));  // k_eh_pick's candidates
-    // gate (ET_PLAN_GATE experiments): recorded after plan step gate_at (1: k_chain_tiles,
-    // 2: k_chain_plan, 3: k_chain_emit) for the caller's stream to wait on
-    auto mark = [&](int at) -> int {
-        if (gate && gate_at == at) ET_HIP_CHECK(hipEventRecord(gate, s));
-        return ET_OK;
-    };
     const int64_t mmax = n / chunk + 2;
     const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
     const int64_t tmax = chain_tiles_max(n, chunk);
@@ -2743,37 +2419,21 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask, eh,
                        w.eh_cand, out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
                        w.chain_tile_col);
-    if (mark(1) != ET_OK) return ET_ERR_HIP;
-    const bool s1 = chain_fed(kFedRegular);  // S = 1 plans: entries = occurrences, no run counts
-    if (!s1)
-        hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
-                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                           w.chain_tile_col, w.chain_tcnt);
-    static const unsigned lat_reg = env_uint("ET_LAT_REG", 0u);
+    hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                       out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                       w.chain_tile_col, w.chain_tcnt);
     hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
-                       w.mlist, w.counters, w.chain_tile0, s1 ? nullptr : w.chain_tcnt,
-                       w.chain_cnt, w.chain_info, w.chains,
-                       s1 ? 0 : 4 | (int)lat_reg << 8);
+                       w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
+                       w.chain_info, w.chains, 4);
     hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
                        w.chain_info, w.chain_e0, w.chain_order);
-    if (mark(2) != ET_OK) return ET_ERR_HIP;
-    if (s1)
-        hipLaunchKernelGGL(k_chain_emit1, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
-                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                           w.chain_tile_col, w.chain_cnt, w.chain_info, w.chain_e0, w.chain_ent,
-                           w.chains);
-    else
-        hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
-                           out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                           w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
-                           w.chain_ent, w.chains);
+    hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
+                       out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
+                       w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
+                       w.chain_ent, w.chains);
     ET_LAUNCH_CHECK("k_chain_emit");
-    if (mark(3) != ET_OK) return ET_ERR_HIP;
-    static const bool check = [] {
-        const char* e = getenv("ET_CHAIN_CHECK");
-        return e && atoi(e) != 0;
-    }();
-    if (check)
+    // ET_CHAIN_CHECK (experiment builds): validate every entry of the plan
+    if (ET_KNOB("ET_CHAIN_CHECK", 0))
         hipLaunchKernelGGL(k_chain_check, dim3(cg), dim3(256), 0, s, pack, ntables, w.counters,
                            w.chain_cnt, w.chain_info, w.chain_ent, w.chains, w.chain_order);
     return ET_OK;
@@ -2884,176 +2544,115 @@ struct VecGroups {
     }
 };
 
-// Single-occurrence columns through k_sgd_singles (ET_SGD_SINGLES=0 turns it off for
-// experiments).
-inline bool sgd_singles() {
-    static const bool v = [] {
-        const char* e = getenv("ET_SGD_SINGLES");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
+// Single-occurrence columns through k_sgd_singles (ET_SGD_SINGLES=0 in an experiment build
+// turns it off) and the chunk pass at 5 waves per SIMD (ET_SGD_OCC5=0: k_sgd_chunks).
+inline bool sgd_singles() { return ET_KNOB("ET_SGD_SINGLES", 1) != 0; }
+inline bool sgd_chunks_occ5() { return ET_KNOB("ET_SGD_OCC5", 1) != 0; }
 
-// k_sgd_chunks5 (5 waves per SIMD) instead of k_sgd_chunks (ET_SGD_OCC5=0/1, for A/B).
-inline bool sgd_chunks_occ5() {
-    static const bool v = [] {
-        const char* e = getenv("ET_SGD_OCC5");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
-
-// The chains of an exact update phase: the side stream of the early chains (null: none)
-// and their column count, the side stream of the regular chains (forked from the caller's
-// stream after the index phase).
+// The chains of an exact update phase: the side streams of the early chains and of the early
+// hot columns (null: none) and their column counts, the side stream of the regular chains
+// (forked from the caller's stream after the index phase).
 struct ChainRun {
-    // reset[i]: the chain list's item counter is reset (early, regular, hot; for tail
-    // launches on the caller's stream after the chunk pass)
-    hipEvent_t reset[3] = {nullptr, nullptr, nullptr};
     hipStream_t ec_side = nullptr;
     uint32_t ec_ncols = 0;
-    hipStream_t eh_side = nullptr;  // the early hot columns (ET_EH)
+    hipStream_t eh_side = nullptr;  // the early hot columns (EH)
     uint32_t eh_ncols = 0;
     hipStream_t side = nullptr;
 };
 
+// Chain workgroups (one CU each): 32 early, 32 early-hot, 128 regular, so the regular chains
+// find free CUs when the index phase releases them instead of waiting for early-chain
+// workgroups (config 4, one box, twice: 256/256 4.62-4.63 ms, 32/128 4.19-4.27, 16/96
+// 4.25-4.29, 64/192 4.42-4.44; profiles/r03/b/ab_exact_knobs.txt; 40/48/64 early-hot
+// workgroups 4.14-4.32 against 4.05-4.08, profiles/r04/ab_exact_grid.txt).
+constexpr unsigned kEcWg = 32, kEhWg = 32, kRegWg = 128;
+// Chain launches on SIMDs of their own (k_sgd_chains_x): bit 0 early, bit 1 regular, bit 2
+// early hot.  The early lists only (config 4, A/B twice on one box: none 4.02-4.11 ms, early
+// 4.015-4.017, regular 4.33-4.34, both 4.35; profiles/r03/e/ab_chain_excl.txt; non-exclusive
+// early hot columns 4.10-4.34 ms, profiles/r04/ab_exact_grid.txt): the regular chains run
+// beside the chunk pass, which needs those SIMDs more.
+constexpr unsigned kChainExcl = 5;
+// The exact mode's chunk pass + singles run at most 512 + 512 grid-stride workgroups: fewer in
+// flight than the split mode's 16384 + 16384 leaves the fabric to the latency-bound chains
+// beside it (config 4, A/B twice on one box: 4.22-4.24 ms at the split mode's grid, 4.05-4.06
+// at 384-768, 4.20 at 256; the split mode itself is faster at its own grid, 3.00 vs 3.61 ms;
+// profiles/r04/ab_exact_grid.txt).
+constexpr unsigned kExactGrid = 512;
+
 // k_sgd_chains on stream `s`: zero the item counter, at most `nb` workgroups.
-template <int MODE, bool NT>
+template <typename T, typename C, int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
-                  const uint32_t* order, const uint2* info, const uint32_t* nocc,
-                  const uint32_t* ent, int ns, float eta32, double eta64, unsigned nhf,
-                  unsigned nb, hipStream_t s, bool excl = false, bool fed = false,
-                  uint32_t lds_req = 0u, hipEvent_t reset_ev = nullptr, bool tail = false) {
-    static const int plain = [] {  // debug: ET_CHAIN_ASM=0 sums the chains in plain C++;
-        // experiments: ET_CHAIN_QUAD=0 walks S = 1 chains with the 64-feature asm loop
-        const char* e = getenv("ET_CHAIN_ASM");
-        const char* q = getenv("ET_CHAIN_QUAD");
-        const char* m = getenv("ET_QUAD_MIN");  // experiments: quad-walk threshold
-        const char* r = getenv("ET_CHAIN_RING");  // S >= 8: the 64-deep ring loop
-        const char* f = getenv("ET_CHAIN_FAKE");  // timing only: every load from row 0
-        const int qmin = m ? atoi(m) : kQuadMinGroups;
-        return (e && atoi(e) == 0 ? 1 : 0) | (q && atoi(q) == 0 ? 2 : 0) |
-               (r && atoi(r) != 0 ? 4 : 0) | (f && atoi(f) != 0 ? 8 : 0) | (qmin << 4);
-    }();
-    // experiments: ET_CHAIN_LDS = KiB reserved per chain workgroup (160: a whole CU)
-    static const uint32_t lds = [] {
-        const char* e = getenv("ET_CHAIN_LDS");
-        const int kb = e ? atoi(e) : 0;
-        return kb > 0 && kb <= 160 ? (uint32_t)kb * 1024u : kChainReserveLds;
-    }();
+                  const uint32_t* order, const uint32_t* ent, int ns, C eta_c, double eta64,
+                  unsigned nb, hipStream_t s, bool excl) {
+    // the quad walk for Float32 S = 1 chains of at least this many 64-entry groups (§9 "The
+    // quad walk": every S = 1 chain 5.56 ms, >= 4 K / 16 K / 64 K / 128 K entries 5.20 / 4.99 /
+    // 4.07-4.16 / 4.36 ms, none 4.48-4.52; profiles/r03/c/ab_quad_min.txt)
+    const uint32_t quad_min = (uint32_t)ET_KNOB("ET_QUAD_MIN", (long long)kQuadMinGroups);
     static const hipError_t attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&k_sgd_chains<MODE, NT>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        reinterpret_cast<const void*>(&k_sgd_chains<T, C, MODE, NT>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
     ET_HIP_CHECK(attr);
     static const hipError_t attr_x = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&k_sgd_chains_x<MODE, NT>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
     ET_HIP_CHECK(attr_x);
-    // plain items start past the helper-fed ones (at 0 when no workgroup is helper-fed);
-    // the helper-fed counter at 0.  A tail launch (more workgroups on the same list, taking
-    // items from the same counter) resets nothing; reset_ev marks the reset for it.
-    if (tail) {
-        if (fed || nhf > 0) return ET_OK;
-    } else {
-        if (nhf > 0)
-            ET_HIP_CHECK(hipMemcpyAsync(counters + kCntNext, counters + kCntHfItems, 4,
-                                        hipMemcpyDeviceToDevice, s));
-        else
-            ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
-        ET_HIP_CHECK(hipMemsetAsync(counters + kCntHfNext, 0, 4, s));
-        if (reset_ev) ET_HIP_CHECK(hipEventRecord(reset_ev, s));
-    }
-    if (fed) {  // every chain planned at S = 1: the fed walk
-        static const hipError_t attr_f = hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&k_sgd_chains_fed<MODE, NT>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFedLds);
-        ET_HIP_CHECK(attr_f);
-        hipLaunchKernelGGL((k_sgd_chains_fed<MODE, NT>), dim3(nb), dim3(64 * (kFedGather + 1)),
-                           kFedLds, s, pack,
-                           ntables, counters, chains, order, ent, ns, eta32, eta64);
-        ET_LAUNCH_CHECK("k_sgd_chains_fed");
-        return ET_OK;
-    }
-    const uint32_t lds_use = lds_req != 0u && lds_req <= lds ? lds_req : lds;
-    if (excl && nhf == 0) {
-        hipLaunchKernelGGL((k_sgd_chains_x<MODE, NT>), dim3(nb), dim3(256), lds_use, s, pack,
-                           ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64,
-                           plain, 0u);
+    ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
+    if (excl) {
+        hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT>), dim3(nb), dim3(256),
+                           kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
+                           eta_c, eta64, quad_min);
         ET_LAUNCH_CHECK("k_sgd_chains_x");
         return ET_OK;
     }
-    hipLaunchKernelGGL((k_sgd_chains<MODE, NT>), dim3(nhf + nb), dim3(256), lds_use, s, pack,
-                       ntables, counters, chains, order, info, nocc, ent, ns, eta32, eta64, plain,
-                       nhf);
+    hipLaunchKernelGGL((k_sgd_chains<T, C, MODE, NT>), dim3(nb), dim3(256), kChainReserveLds, s,
+                       pack, ntables, counters, chains, order, ent, ns, eta_c, eta64, quad_min);
     ET_LAUNCH_CHECK("k_sgd_chains");
     return ET_OK;
 }
 
-// The update phase of an exact Float32 call: the early chains (side stream 1, already
-// planned) and the regular chains (side stream 2) in k_sgd_chains, the chunk pass over
-// single-chunk columns + the singles in one launch per capacity group on the caller's
-// stream, then the generic tables' single-chunk columns.  No partial sums, no combine.
-template <int MODE, bool NT>
-int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
-                     int64_t n, int pdim, uint32_t sent, float eta32, double eta64,
-                     const VecGroups& vg, bool any_generic, hipStream_t s, unsigned grid,
-                     ChainRun cr) {
-    const int ns = (pdim + 63) / 64;
-    // The chunk pass + singles of the exact mode run at most 512 + 512 grid-stride
-    // workgroups: fewer in flight than the split mode's 16384 + 16384 leaves the fabric to
-    // the latency-bound chains beside it (config 4, A/B twice on one box: 4.22-4.24 ms at
-    // the split mode's grid, 4.05-4.06 at 384-768, 4.20 at 256; the split mode itself is
-    // faster at its own grid, 3.00 vs 3.61 ms; profiles/r04/ab_exact_grid.txt).
-    // ET_EXACT_GRID overrides (experiments).
-    static const unsigned xcap = env_uint("ET_EXACT_GRID", 512u);
-    grid = grid < xcap ? grid : xcap;
-    // chain workgroups (one CU each): 32 early, 128 regular, so the regular chains find
-    // free CUs when the index phase releases them instead of waiting for early-chain
-    // workgroups (config 4, one box, twice: 256/256 4.62-4.63 ms, 32/128 4.19-4.27,
-    // 16/96 4.25-4.29, 64/192 4.42-4.44; profiles/r03/b/ab_exact_knobs.txt).
-    // ET_EC_WG / ET_CHAIN_WG override (experiments).
-    static const unsigned ec_wg = env_uint("ET_EC_WG", 32u), reg_wg = env_uint("ET_CHAIN_WG", 128u);
-    // chain launches on SIMDs of their own (k_sgd_chains_x): bit 0 early, bit 1 regular.
-    // The early chains only (config 4, A/B twice on one box: none 4.02-4.11 ms, early
-    // 4.015-4.017, regular 4.33-4.34, both 4.35; profiles/r03/e/ab_chain_excl.txt): the
-    // regular chains run beside the chunk pass, which needs those SIMDs more.
-    // Bit 2: the early hot columns (ET_EH) too.
-    static const unsigned excl = [] {
-        const char* e = getenv("ET_CHAIN_EXCL");
-        return e ? (unsigned)atoi(e) & 7u : 5u;
-    }();
+// The three chain lists of an exact update phase on their side streams: the early chains and
+// the early hot columns (already planned) and the regular chains.
+template <typename T, typename C, int MODE, bool NT>
+int launch_chain_lists(const UpdatePack& pack, int ntables, UpdateWs& w, int ns, C eta_c,
+                       double eta64, const ChainRun& cr) {
+    const unsigned excl = (unsigned)ET_KNOB("ET_CHAIN_EXCL", kChainExcl);
     int rc;
     if (cr.ec_side) {
         const int64_t items = (int64_t)cr.ec_ncols * ns;
-        const unsigned eb = (unsigned)(cdiv64(items, 4) < ec_wg ? cdiv64(items, 4) : ec_wg);
-        // helper-fed pairs (k_sgd_chains' first nhf workgroups): kept for experiments but
-        // off — their helper was latency-bound, and the plain items are numbered per
-        // quarter (kQuadItems) since the quad walk
-        const unsigned hf_wg = 0u;
-        rc = launch_chains<MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
-                                     w.ec.info, w.ec.nocc, w.ec.ent, ns, eta32, eta64, hf_wg, eb,
-                                     cr.ec_side, (excl & 1u) != 0, chain_fed(kFedEarly), 0u,
-                                     cr.reset[0]);
+        const unsigned wg = (unsigned)ET_KNOB("ET_EC_WG", kEcWg);
+        const unsigned eb = (unsigned)(cdiv64(items, 4) < wg ? cdiv64(items, 4) : wg);
+        rc = launch_chains<T, C, MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
+                                           w.ec.ent, ns, eta_c, eta64, eb, cr.ec_side,
+                                           (excl & 1u) != 0);
         if (rc != ET_OK) return rc;
     }
     if (cr.eh_side) {
-        static const unsigned eh_wg = env_uint("ET_EH_WG", 32u);
-        // ET_EH_LDS: KiB reserved per hot-column workgroup (experiments; default the chain
-        // launches' one-workgroup-per-CU reservation)
-        static const unsigned eh_lds = env_uint("ET_EH_LDS", 0u) * 1024u;
         const int64_t items = (int64_t)cr.eh_ncols * ns;
-        const unsigned eb = (unsigned)(cdiv64(items, 4) < eh_wg ? cdiv64(items, 4) : eh_wg);
-        rc = launch_chains<MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
-                                     w.eh.info, w.eh.nocc, w.eh.ent, ns, eta32, eta64, 0u, eb,
-                                     cr.eh_side, (excl & 4u) != 0, chain_fed(kFedHot),
-                                     eh_lds <= 160u * 1024u ? eh_lds : 0u, cr.reset[2]);
+        const unsigned wg = (unsigned)ET_KNOB("ET_EH_WG", kEhWg);
+        const unsigned eb = (unsigned)(cdiv64(items, 4) < wg ? cdiv64(items, 4) : wg);
+        rc = launch_chains<T, C, MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
+                                           w.eh.ent, ns, eta_c, eta64, eb, cr.eh_side,
+                                           (excl & 4u) != 0);
         if (rc != ET_OK) return rc;
     }
-    rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
-                                 w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u, reg_wg,
-                                 cr.side, (excl & 2u) != 0, chain_fed(kFedRegular), 0u,
-                                 cr.reset[1]);
+    return launch_chains<T, C, MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
+                                         w.chain_ent, ns, eta_c, eta64,
+                                         (unsigned)ET_KNOB("ET_CHAIN_WG", kRegWg), cr.side,
+                                         (excl & 2u) != 0);
+}
+
+// The update phase of an exact Float32 call: the chain lists on the side streams, the chunk
+// pass over single-chunk columns + the singles in one launch per capacity group on the
+// caller's stream, then the generic tables' single-chunk columns.  No partial sums, no
+// combine.
+template <int MODE, bool NT>
+int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
+                     int pdim, uint32_t sent, float eta32, double eta64, const VecGroups& vg,
+                     bool any_generic, hipStream_t s, unsigned grid, const ChainRun& cr) {
+    const int ns = (pdim + 63) / 64;
+    const unsigned xcap = (unsigned)ET_KNOB("ET_EXACT_GRID", kExactGrid);
+    grid = grid < xcap ? grid : xcap;
+    int rc = launch_chain_lists<float, float, MODE, NT>(pack, ntables, w, ns, eta32, eta64, cr);
     if (rc != ET_OK) return rc;
 #define ET_SGD_EXACT(DD)                                                                       \
     case DD:                                                                                   \
@@ -3082,33 +2681,23 @@ int launch_sgd_exact(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
                            pdim, sent, eta32, eta64, 1);
         ET_LAUNCH_CHECK("k_sgd_chunks_generic");
     }
-    // Tail workgroups (ET_TAIL_EC / _EH / _REG, experiments): more workgroups for a chain
-    // list on the caller's stream, so they start when the chunk pass ends and take the
-    // list's remaining items from the same counter (the CUs the pass held are idle then)
-    static const unsigned tail_ec = env_uint("ET_TAIL_EC", 0u), tail_eh = env_uint("ET_TAIL_EH", 0u),
-                          tail_reg = env_uint("ET_TAIL_REG", 0u);
-    if (cr.ec_side && tail_ec && cr.reset[0]) {
-        ET_HIP_CHECK(hipStreamWaitEvent(s, cr.reset[0], 0));
-        rc = launch_chains<MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
-                                     w.ec.info, w.ec.nocc, w.ec.ent, ns, eta32, eta64, 0u, tail_ec,
-                                     s, (excl & 1u) != 0, chain_fed(kFedEarly), 0u, nullptr, true);
-        if (rc != ET_OK) return rc;
-    }
-    if (cr.eh_side && tail_eh && cr.reset[2]) {
-        ET_HIP_CHECK(hipStreamWaitEvent(s, cr.reset[2], 0));
-        rc = launch_chains<MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
-                                     w.eh.info, w.eh.nocc, w.eh.ent, ns, eta32, eta64, 0u, tail_eh,
-                                     s, (excl & 4u) != 0, chain_fed(kFedHot), 0u, nullptr, true);
-        if (rc != ET_OK) return rc;
-    }
-    if (tail_reg && cr.reset[1]) {
-        ET_HIP_CHECK(hipStreamWaitEvent(s, cr.reset[1], 0));
-        rc = launch_chains<MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
-                                     w.chain_info, nullptr, w.chain_ent, ns, eta32, eta64, 0u,
-                                     tail_reg, s, (excl & 2u) != 0, chain_fed(kFedRegular), 0u,
-                                     nullptr, true);
-        if (rc != ET_OK) return rc;
-    }
+    return ET_OK;
+}
+
+// The exact update phase of Float64 / Float16 / BFloat16 tables: the same three chain lists
+// (walked by chain_walk_wide in the accumulator type) beside the generic chunk pass over the
+// single-chunk columns (one wave per chunk, serial in occurrence order).
+template <typename T, typename C, int MODE, bool NT>
+int launch_sgd_exact_generic(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
+                             int pdim, uint32_t sent, C eta_c, double eta64, hipStream_t s,
+                             unsigned grid, const ChainRun& cr) {
+    int rc = launch_chain_lists<T, C, MODE, NT>(pack, ntables, w, (pdim + 63) / 64, eta_c, eta64,
+                                                cr);
+    if (rc != ET_OK) return rc;
+    hipLaunchKernelGGL((k_sgd_chunks_generic<T, C, MODE, NT>), dim3(grid), dim3(256), 0, s, pack,
+                       ntables, gr.keys, gr.vals, w.recs, w.counters,
+                       reinterpret_cast<C*>(w.partials), pdim, sent, eta_c, eta64, 1);
+    ET_LAUNCH_CHECK("k_sgd_chunks_generic");
     return ET_OK;
 }
 
@@ -3116,11 +2705,16 @@ template <typename T, typename C, int MODE, bool NT>
 int launch_sgd_typed(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, C eta_c, double eta64,
                      const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl, unsigned grid, bool chain, int64_t n, ChainRun cr) {
-    if constexpr (__is_same(T, float)) {
-        if (chain)
-            return launch_sgd_exact<MODE, NT>(pack, ntables, gr, w, n, pdim, sent, eta_c, eta64, vg,
+                     const HotList& hl, unsigned grid, bool chain, const ChainRun& cr) {
+    if (chain) {
+        if constexpr (__is_same(T, float))
+            return launch_sgd_exact<MODE, NT>(pack, ntables, gr, w, pdim, sent, eta_c, eta64, vg,
                                               any_generic, s, grid, cr);
+        else
+            return launch_sgd_exact_generic<T, C, MODE, NT>(pack, ntables, gr, w, pdim, sent,
+                                                            eta_c, eta64, s, grid, cr);
+    }
+    if constexpr (__is_same(T, float)) {
         const bool singles = sgd_singles();
         // combine workgroups of k_sgd_tail: a quarter of one resident wave of workgroups,
         // so the singles start at once beside them
@@ -3205,11 +2799,10 @@ template <typename T, typename C>
 int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, UpdateWs& w,
                      uint32_t chunk, int pdim, uint32_t sent, double eta_c, double eta64,
                      int mode, bool nt, const VecGroups& vg, bool any_generic, hipStream_t s,
-                     const HotList& hl, unsigned grid, bool chain = false, int64_t n = 0,
-                     ChainRun cr = ChainRun{}) {
+                     const HotList& hl, unsigned grid, bool chain, const ChainRun& cr) {
 #define ET_SGD_CALL(M, NTV)                                                                \
     return launch_sgd_typed<T, C, M, NTV>(pack, ntables, gr, w, chunk, pdim, sent, (C)eta_c, \
-                                          eta64, vg, any_generic, s, hl, grid, chain, n, cr)
+                                          eta64, vg, any_generic, s, hl, grid, chain, cr)
     if (mode == 0) {
         if (nt) ET_SGD_CALL(0, true);
         ET_SGD_CALL(0, false);
@@ -3226,11 +2819,6 @@ int launch_sgd_dtype(const UpdatePack& pack, int ntables, const Grouped& gr, Upd
 // 256..16384 — 16384 measured 3% faster than 4096 on the config-4 batch (3.72 vs 3.84
 // ms), and small batches launch fewer idle workgroups.
 inline unsigned sgd_grid(int64_t n) {
-    static const int forced = [] {
-        const char* e = getenv("ET_SGD_GRID");  // experiments: a fixed grid
-        return e ? atoi(e) : 0;
-    }();
-    if (forced > 0) return (unsigned)forced;
     const int64_t g = cdiv64(n, 2048);
     return (unsigned)(g < 256 ? 256 : g > 16384 ? 16384 : g);
 }
@@ -3322,66 +2910,41 @@ inline EhMap eh_map(const EcList& eh) {
     return m;
 }
 
-// Exact Float32 mode: columns of more occurrences than this are serial chains
-// (k_sgd_chains), the rest single chunks of the chunk pass (ET_EXACT_CHUNK, experiments).
+// Exact mode: columns of more occurrences than this are serial chains (k_sgd_chains), the
+// rest single chunks of the chunk pass.
 constexpr uint32_t kExactChunk = ET_SGD_CHUNK;
-inline uint32_t exact_chunk() {
-    static const uint32_t v = [] {
-        const char* e = getenv("ET_EXACT_CHUNK");
-        const int x = e ? atoi(e) : 0;
-        return x >= (int)ET_SGD_CHUNK ? (uint32_t)x : kExactChunk;
-    }();
-    return v;
-}
 
-// ET_EC=0 plans every chain from the sorted pairs (experiments).
-inline bool ec_enabled() {
-    static const bool v = [] {
-        const char* e = getenv("ET_EC");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
-// Two side streams per device (highest priority) for the exact mode's chains: stream 0
-// takes the early chains (forked from the caller's stream at the start of the call), stream
-// 1 the regular ones (forked after the index phase).  Both are joined back into the
-// caller's stream inside the same library call, so a HIP graph capture of the caller's
-// stream captures every branch.  The fork/join events are shared, so a call that uses
-// the side streams holds `mu` from its first fork to its last join.
+// Four library streams per device (highest priority) carry ALL of an exact-mode call's
+// device work: stream 3 the index phase and the chunk pass (what a single-stream call runs
+// on the caller's stream), stream 0 the early chains, stream 2 the early hot columns (both
+// planned from the index arrays, forked at the start of the call), stream 1 the regular
+// chains (forked from stream 3 after the index phase).  The caller's stream only forks them
+// at the start and joins them at the end, inside the same library call, so a HIP graph
+// capture of the caller's stream captures every branch.  The fork/join events are shared,
+// so a call that uses the side streams holds `mu` from its first fork to its last join.
+//
+// Why the caller's stream carries no work: a process's hardware queues
+// share the command processor's pipes, and a queue whose chain launch is waiting for whole
+// CUs (one chain workgroup per CU, SIMDs of its own) holds up the dispatch of every other
+// queue on its pipe.  Round 4 ran the index phase on the caller's queue; whenever another
+// queue had been opened before the library's side streams (a torch.cuda.graph capture, or
+// ANY stream that had run a kernel — tools/capture_effect.py: dummy1..4, hidummy1,
+// capture), one side queue landed on the caller's pipe and the index phase's kernels ran
+// 2-4x longer (k_build_keys 174 -> 384 us, scans 5-14 -> 40-56 us; the update 4.07 ->
+// 5.15-5.34 ms; profiles/r05/capture_effect.txt).  With one side stream opened after the
+// library's, on a different pipe, nothing slowed (capture_after: 4.08 ms).  Now the four
+// streams that carry work are opened together, one after another (init() touches each
+// with an event record, which acquires its hardware queue), so they take consecutive
+// queues, and the caller's queue idles during the call.
 struct SideStreams {
-    static constexpr int kN = 3;  // early chains, regular chains, early hot columns (ET_EH)
+    static constexpr int kN = 4;  // early chains, regular chains, early hot columns, work
+    static constexpr int kEc = 0, kReg = 1, kEh = 2, kWork = 3;
     std::mutex mu;
-    hipStream_t st[kN] = {nullptr, nullptr, nullptr};
-    hipEvent_t fork[kN] = {nullptr, nullptr, nullptr}, join[kN] = {nullptr, nullptr, nullptr};
+    hipStream_t st[kN] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t fork[kN] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t join[kN] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t cand = nullptr;  // the hot-column candidates are picked (k_eh_pick)
-    hipEvent_t gate = nullptr;  // ET_PLAN_GATE: a step of the regular plan is done
-    hipEvent_t reset[kN] = {nullptr, nullptr, nullptr};  // a chain list's counter is reset
 };
-
-// The side streams' priority: the device's greatest (default), or ET_SIDE_PRIO=0 the
-// least (experiments).
-inline int side_prio(int least, int greatest) {
-    const char* e = getenv("ET_SIDE_PRIO");
-    return e && atoi(e) == 0 ? least : greatest;
-}
-
-// ET_SIDE_CUMASK=1 (experiments): the side streams with a full CU mask, which gives each a
-// hardware queue of its own.
-inline hipError_t side_stream_create(hipStream_t* st, int least, int greatest) {
-    const char* e = getenv("ET_SIDE_CUMASK");
-    if (e && atoi(e) != 0) {
-        int dev = 0, ncu = 0;
-        hipError_t r = hipGetDevice(&dev);
-        if (r == hipSuccess) r = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (r != hipSuccess) return r;
-        uint32_t mask[16];
-        const int words = (ncu + 31) / 32 < 16 ? (ncu + 31) / 32 : 16;
-        for (int k = 0; k < words; ++k) mask[k] = 0xffffffffu;
-        return hipExtStreamCreateWithCUMask(st, (uint32_t)words, mask);
-    }
-    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, side_prio(least, greatest));
-}
 
 inline SideStreams* side_streams() {
     static SideStreams streams[64];
@@ -3396,31 +2959,33 @@ inline SideStreams* side_streams() {
         for (int i = 0; i < SideStreams::kN; ++i)
             if ((!ss.fork[i] && hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming)) ||
                 (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
-                (!ss.st[i] && side_stream_create(&ss.st[i], least, greatest)))
+                (!ss.st[i] &&
+                 hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking, greatest)))
                 return nullptr;
-        if (hipEventCreateWithFlags(&ss.gate, hipEventDisableTiming) != hipSuccess) return nullptr;
+        // acquire the four hardware queues back to back (an event record is a packet on
+        // the stream's queue), so they are consecutive whatever the process opened before
         for (int i = 0; i < SideStreams::kN; ++i)
-            if (!ss.reset[i] && hipEventCreateWithFlags(&ss.reset[i], hipEventDisableTiming) != hipSuccess)
-                return nullptr;
+            if (hipEventRecord(ss.join[i], ss.st[i]) != hipSuccess) return nullptr;
         if (hipEventCreateWithFlags(&ss.cand, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
     return &ss;
 }
 
-// fork(i): side stream i waits for everything the caller's stream has queued so far;
-// the destructor joins every forked side stream (every return path of et_sparse_sgd).
+// fork(i, from): side stream i waits for everything `from` (default: the caller's stream)
+// has queued so far; the destructor joins every forked side stream into the caller's stream
+// (every return path of et_sparse_sgd).
 struct SideFork {
     SideStreams* ss = nullptr;
     hipStream_t main = nullptr;
     std::unique_lock<std::mutex> lk;
-    bool forked[SideStreams::kN] = {false, false, false};
+    bool forked[SideStreams::kN] = {false, false, false, false};
     SideFork(SideStreams* s, hipStream_t m) : ss(s), main(m) {
         if (ss) lk = std::unique_lock<std::mutex>(ss->mu);
     }
-    hipStream_t fork(int i) {
+    hipStream_t fork(int i, hipStream_t from = nullptr) {
         if (!ss) return nullptr;
         if (!forked[i]) {
-            if (hipEventRecord(ss->fork[i], main) != hipSuccess ||
+            if (hipEventRecord(ss->fork[i], from ? from : main) != hipSuccess ||
                 hipStreamWaitEvent(ss->st[i], ss->fork[i], 0) != hipSuccess)
                 return nullptr;
             forked[i] = true;
@@ -3445,8 +3010,8 @@ inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chu
     const uint32_t M = ec.col0[ec.n];
     uint32_t* cand = const_cast<uint32_t*>(cand_c);
     if (ec.hot) {
-        // ET_EH_MIN: the expected occurrences of a candidate (tests: small batches)
-        static const uint32_t min_occ = env_uint("ET_EH_MIN", kEhMinOcc);
+        // ET_EH_MIN (experiment builds): the expected occurrences of a candidate
+        const uint32_t min_occ = (uint32_t)ET_KNOB("ET_EH_MIN", (long long)kEhMinOcc);
         hipLaunchKernelGGL(k_eh_pick, dim3(ec.n), dim3(1024), 0, s, pack, ec, min_occ, cand);
         ET_LAUNCH_CHECK("k_eh_pick");
         if (cand_ready) ET_HIP_CHECK(hipEventRecord(cand_ready, s));
@@ -3454,13 +3019,10 @@ inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chu
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
     hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.stats,
                        cand_c);
-    static const unsigned lat_eh = env_uint("ET_LAT_EH", 0u), lat_ec = env_uint("ET_LAT_EC", 0u);
     hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
-                       w.stats, w.boff, w.cnt, w.nocc, w.info, w.chains, w.ent, w.counters,
-                       chain_fed(ec.hot ? kFedHot : kFedEarly) ? 0
-                                       : 4 | (int)(ec.hot ? lat_eh : lat_ec) << 8,
+                       w.stats, w.boff, w.cnt, w.nocc, w.info, w.chains, w.ent, w.counters, 4,
                        cand_c);
-    hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.info, w.nocc, ns, w.order,
+    hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.info, ns, w.order,
                        w.counters);
     hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.boff,
                        w.info, w.ent, cand_c);
@@ -3531,23 +3093,20 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     if (rc != ET_OK) return rc;
     if (n == 0) return ET_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const bool exact_forced = (flags & ET_FLAG_EXACT_UPDATE) != 0;
-    // Exact Float32: columns longer than a chunk are summed as serial chains (k_chain_*,
-    // k_sgd_exact), whose entries hold a 24-bit bag and whose loop addresses the gradient
-    // by a 32-bit byte offset (bag * ld * 4 from 24-bit factors).  Other exact calls keep
-    // every column in one chunk (a chunk spans a whole segment).
-    bool chain = (exact_forced || (flags & ET_FLAG_EXACT_IF_FAST)) && dtype == ET_F32;
+    // Exact mode (ET_FLAG_EXACT_UPDATE, and since ABI v9 ET_FLAG_EXACT_IF_FAST too: the chain
+    // path now covers every element type and gradient size): every column's gradient summed
+    // serially in occurrence order, as the reference does.  Columns longer than a chunk are
+    // serial chains (k_chain_*, k_sgd_chains) whose entries hold a 24-bit bag, so a batch of
+    // 2^24 bags or more keeps every column in one chunk instead (a chunk then spans a whole
+    // segment: exact, one wave per column).
+    const bool exact = (flags & (ET_FLAG_EXACT_UPDATE | ET_FLAG_EXACT_IF_FAST)) != 0;
+    bool chain = exact;
     for (int t = 0; t < ntables && chain; ++t)
-        if (descs[t].batch >= (1 << 24) || descs[t].ld_delta >= (1 << 22) ||
-            (uint64_t)descs[t].batch * (uint64_t)descs[t].ld_delta >= (1ull << 30))
-            chain = false;
-    // ET_FLAG_EXACT_IF_FAST: exact only where the chains run (decided from the descriptors
-    // alone, so an INDEX_ONLY and its APPLY_ONLY call agree)
-    const bool exact = exact_forced || chain;
-    // exact chain mode: a column of at most kExactChunk occurrences is one chunk of the
-    // chunk pass (a lane group's serial sum over full 512-byte rows), a longer one a chain
+        if (descs[t].batch >= (1 << 24)) chain = false;
+    // chain mode: a column of at most kExactChunk occurrences is one chunk of the chunk pass
+    // (a lane group's serial sum), a longer one a chain
     const uint32_t chunk = exact && !chain ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff)
-                           : chain          ? et::exact_chunk()
+                           : chain          ? et::kExactChunk
                                             : et::kChunk;
     int nhot;
     int64_t hb, hbytes;
@@ -3609,18 +3168,23 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
             hl.soff[hl.n] = soff[t];
             hl.t[hl.n++] = t;
         }
-    // exact Float32: the chains run on two side streams — the early chains (small tables,
-    // planned from the index arrays at the start of the index phase) from the start of the
-    // call, the regular ones once the index phase has planned them
-    const bool use_ec = chain && ec.n > 0 && et::ec_enabled();
-    const bool use_eh = chain && eh.n > 0 && et::ec_enabled();  // eh.n > 0 only under ET_EH
+    // exact mode: the chains run on three side streams — the early chains (small tables) and
+    // the early hot columns (the big tables' hottest, sampled), both planned from the index
+    // arrays from the start of the call, and the regular ones once the index phase has
+    // planned them
+    const bool use_ec = chain && ec.n > 0;
+    const bool use_eh = chain && eh.n > 0;
     const et::EhMap ehm = et::eh_map(use_eh ? eh : et::EcList{});
     et::SideStreams* sides = chain ? et::side_streams() : nullptr;
     if (chain && !sides) return et::fail(ET_ERR_HIP, "sparse SGD: side streams unavailable");
     et::SideFork fork(sides, s);
+    if (chain) {  // the call's main-line work moves to the library's work stream
+        s = fork.fork(et::SideStreams::kWork);
+        if (!s) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
+    }
     hipStream_t ec_side = nullptr;
     if (use_ec) {
-        ec_side = fork.fork(0);
+        ec_side = fork.fork(et::SideStreams::kEc);
         if (!ec_side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
         if (!apply_only) {
             rc = et::launch_ec_plan(pack, ec, chunk, w.ec, nullptr, (pdim + 63) / 64, ec_side);
@@ -3629,7 +3193,7 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     }
     hipStream_t eh_side = nullptr;
     if (use_eh) {
-        eh_side = fork.fork(2);
+        eh_side = fork.fork(et::SideStreams::kEh);
         if (!eh_side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
         if (!apply_only) {
             rc = et::launch_ec_plan(pack, eh, chunk, w.eh, w.eh_cand, (pdim + 63) / 64, eh_side,
@@ -3647,37 +3211,26 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     }
     et::ChainRun cr;
     if (chain) {
-        if (sides)
-            for (int i = 0; i < 3; ++i) cr.reset[i] = sides->reset[i];
         cr.ec_side = ec_side;
         cr.ec_ncols = use_ec ? ec.col0[ec.n] : 0u;
         cr.eh_side = eh_side;
         cr.eh_ncols = use_eh ? eh.col0[eh.n] : 0u;
         // the regular chains' plan: on their side stream beside the chunk pass (default), or
-        // on the caller's stream before it (ET_PLAN_SIDE=0: the chains start earlier, the
-        // chunk pass later)
-        static const bool plan_side = [] {
-            const char* e = getenv("ET_PLAN_SIDE");
-            return e ? atoi(e) != 0 : true;
-        }();
+        // on the caller's stream before it (ET_PLAN_SIDE=0 in an experiment build: the chains
+        // start earlier, the chunk pass later; 4.13-4.16 vs 4.07 ms, round 4)
+        const bool plan_side = ET_KNOB("ET_PLAN_SIDE", 1) != 0;
         if (!apply_only && !plan_side) {
             rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, s,
                                        use_ec ? ec.mask : 0u, ehm, sides->cand);
             if (rc != ET_OK) return rc;
         }
-        cr.side = fork.fork(1);  // after the index phase's chunk records (and the plan)
+        // after the index phase's chunk records (and the plan), on the work stream
+        cr.side = fork.fork(et::SideStreams::kReg, s);
         if (!cr.side) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
         if (!apply_only && plan_side) {
-            // ET_PLAN_GATE=1/2/3 (experiments): the chunk pass waits for the plan's
-            // k_chain_tiles / k_chain_plan / k_chain_emit, whose single-workgroup kernels
-            // otherwise wait for CUs held by the chunk pass's persistent workgroups
-            static const int gate_at = (int)et::env_uint("ET_PLAN_GATE", 0u);
             rc = et::launch_chain_plan(pack, ntables, n, sent, chunk, w, gr, cr.side,
-                                       use_ec ? ec.mask : 0u, ehm, sides->cand, sides->gate,
-                                       gate_at);
+                                       use_ec ? ec.mask : 0u, ehm, sides->cand);
             if (rc != ET_OK) return rc;
-            if (gate_at >= 1 && gate_at <= 3)
-                ET_HIP_CHECK(hipStreamWaitEvent(s, sides->gate, 0));
         }
     }
     if (index_only) return ET_OK;
@@ -3689,24 +3242,24 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     switch (dtype) {
         case ET_F32:
             return et::launch_sgd_dtype<float, float>(pack, ntables, gr, w, chunk, pdim, sent,
-                                                      eta_c, eta, mode, nt, vg,
-                                                      any_generic, s, hl, grid, chain, n, cr);
+                                                      eta_c, eta, mode, nt, vg, any_generic, s,
+                                                      hl, grid, chain, cr);
         case ET_F64:
             return et::launch_sgd_dtype<double, double>(pack, ntables, gr, w, chunk, pdim, sent,
-                                                         eta_c, eta, mode, nt, vg,
-                                                         any_generic, s, hl, grid);
+                                                         eta_c, eta, mode, nt, vg, any_generic,
+                                                         s, hl, grid, chain, cr);
         case ET_BF16:
             return et::launch_sgd_dtype<__bf16, float>(pack, ntables, gr, w, chunk, pdim, sent,
-                                                       eta_c, eta, mode, nt, vg,
-                                                       any_generic, s, hl, grid);
+                                                       eta_c, eta, mode, nt, vg, any_generic, s,
+                                                       hl, grid, chain, cr);
         default:  // ET_F16
             if (flags & ET_FLAG_F16_FP32_ACC)
                 return et::launch_sgd_dtype<_Float16, float>(pack, ntables, gr, w, chunk, pdim,
                                                              sent, eta_c, eta, mode, nt, vg,
-                                                             any_generic, s, hl, grid);
+                                                             any_generic, s, hl, grid, chain, cr);
             return et::launch_sgd_dtype<_Float16, _Float16>(pack, ntables, gr, w, chunk, pdim,
                                                             sent, eta_c, eta, mode, nt, vg,
-                                                            any_generic, s, hl, grid);
+                                                            any_generic, s, hl, grid, chain, cr);
     }
 }
 

@@ -27,7 +27,8 @@ ET_FLAG_SGD_APPLY_ONLY = 64
 ET_FLAG_SGD_HOT_PASS = 128
 ET_MAX_TABLES_PER_LAUNCH = 32
 ET_SGD_CHUNK = 256  # include/embtab.h: occurrences per chunk of the non-exact SGD
-ET_ABI_VERSION = 8
+ET_ABI_VERSION = 9
+ET_LOOKUP_QUEUE_BYTES = 128  # include/embtab.h: et_maplookup_prealloc_q queue block
 ET_MAX_PEERS = 16
 ET_PLAN_TABLEWISE, ET_PLAN_FEATUREWISE = 0, 1
 ET_EXCHANGE_ALLGATHER, ET_EXCHANGE_ALLTOALL = 0, 1
@@ -49,6 +50,7 @@ EXPORTS = (
     "et_gather",
     "et_pooled_sum",
     "et_maplookup_prealloc",
+    "et_maplookup_prealloc_q",
     "et_maplookup_prealloc_to",
     "et_sgd_workspace_size",
     "et_sparse_sgd",
@@ -151,6 +153,7 @@ def load() -> ctypes.CDLL:
         "et_gather": ([c_int, vp, i64, i64, i32, vp, i64, vp, i64, u32, vp], c_int),
         "et_pooled_sum": ([c_int, vp, i64, i64, i32, vp, i32, i64, i64, vp, i64, u32, vp], c_int),
         "et_maplookup_prealloc": ([c_int, vp, i32, i64, vp, i64, u32, vp], c_int),
+        "et_maplookup_prealloc_q": ([c_int, vp, i32, i64, vp, i64, u32, vp, vp], c_int),
         "et_maplookup_prealloc_to": ([c_int, c_int, vp, i32, i64, vp, i64, u32, vp], c_int),
         "et_sgd_workspace_size": ([vp, i32, vp], c_int),
         "et_sparse_sgd": ([c_int, vp, i32, dbl, u32, vp, i64, vp], c_int),

@@ -15,6 +15,7 @@ path.  Names with a trailing underscore are Julia's bang functions
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import torch
 
@@ -216,6 +217,26 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
     return PreallocationPlan(strategy, dst, tables, Is, nontemporal, f16_fp32_acc)()
 
 
+# Queue blocks of the per-XCD work-queue schedule (et_maplookup_prealloc_q), one per
+# (device, stream, thread): calls that share a block are ordered by their stream.  Zeroed once
+# on that stream when made; every launch leaves its block zero again.
+_QUEUE_BLOCKS: dict = {}
+
+
+def _queue_block(device: torch.device, stream: int):
+    """The queue block for launches on `stream`, or None while the stream is capturing a
+    HIP graph (the captured launch keeps the static stripe schedule: a block allocated
+    during a capture would be graph-private memory)."""
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    key = (device.index, stream, threading.get_ident())
+    q = _QUEUE_BLOCKS.get(key)
+    if q is None:
+        q = torch.zeros(_lib.ET_LOOKUP_QUEUE_BYTES // 4, dtype=torch.int32, device=device)
+        _QUEUE_BLOCKS[key] = q
+    return q
+
+
 class PreallocationPlan:
     """``maplookup!(PreallocationStrategy(k), dst, tables, I)`` with the descriptors
     validated and built once for fixed tables, index buffers and destination: each
@@ -274,9 +295,10 @@ class PreallocationPlan:
         dst = self._dst
         stream = _lib.stream_handle(dst.device)
         if self._src == self._dst_t:
-            _lib.check(self._lib.et_maplookup_prealloc(
+            q = _queue_block(dst.device, stream)
+            _lib.check(self._lib.et_maplookup_prealloc_q(
                 self._src, ctypes.addressof(self._descs), self._n, self._B, dst.data_ptr(),
-                self._ld, self._flags, stream))
+                self._ld, self._flags, q.data_ptr() if q is not None else None, stream))
         else:  # PreallocationStrategy{U}: sums in the table type, converted on the store
             _lib.check(self._lib.et_maplookup_prealloc_to(
                 self._src, self._dst_t, ctypes.addressof(self._descs), self._n, self._B,

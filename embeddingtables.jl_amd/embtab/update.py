@@ -285,7 +285,7 @@ def _sgd_flags(fused: bool, nontemporal: bool, f64_alpha: bool = False,
         flags |= _lib.ET_FLAG_SGD_UNFUSED
         if f64_alpha:
             flags |= _lib.ET_FLAG_SGD_F64_ALPHA
-    if exact is None:  # exact where the serial-chain path runs (Float32), split otherwise
+    if exact is None:  # the bindings' default: exact (the serial-chain path, every dtype)
         flags |= _lib.ET_FLAG_EXACT_IF_FAST
     elif exact:
         flags |= _lib.ET_FLAG_EXACT_UPDATE
@@ -322,14 +322,13 @@ def _sparse_sgd(descs, eta: float, flags: int, device, dtype=torch.float32):
                                flags, ws.data_ptr(), ws.numel(), _lib.stream_handle(device)))
 
 
-# The exact update (ET_FLAG_EXACT_UPDATE: every column's gradient summed serially in the
-# reference's order, src/sparseupdate.jl:110-127 — bit-identical) is the default wherever it
-# has its fast serial-chain path: EXACT_DEFAULT = None passes ET_FLAG_EXACT_IF_FAST, which the
-# library resolves per call to exact for Float32 tables (batch < 2^24, batch * ld < 2^30) and
-# to the split mode otherwise — exact Float64 / Float16 / BFloat16 updates would sum a hot
-# column in one wave, one occurrence at a time (835 K serial loads for config 4's hottest
-# column).  exact=True forces the exact mode for any dtype; exact=False selects the split
-# mode (columns longer than ET_SGD_CHUNK summed as ordered partial sums).
+# The exact update (every column's gradient summed serially in the reference's order,
+# src/sparseupdate.jl:110-127 — bit-identical) is the default: EXACT_DEFAULT = None passes
+# ET_FLAG_EXACT_IF_FAST, which since ABI v9 is exact for every element type and gradient size
+# (the serial-chain path: the hand-scheduled Float32 loop, or 64-bit addressed chains for a
+# gradient beyond its 32-bit offsets and for Float64 / Float16 / BFloat16 tables).
+# exact=True is the same; exact=False selects the split mode (columns longer than
+# ET_SGD_CHUNK summed as ordered partial sums).
 EXACT_DEFAULT = None
 
 
@@ -344,12 +343,11 @@ def update_(*args, nontemporal: bool | None = None, exact: bool | None = None,
     * ``update_(table, grad, indexer_or_view, alpha, [nontemporal])`` — update from a
       prebuilt Indexer / IndexerView range (:46-154).
 
-    ``exact=True`` sums every column's gradient serially (bit-identical to the reference
-    even for hot columns: longer columns run as serial chains beside the chunk pass);
+    ``exact=True`` (and the default, EXACT_DEFAULT = None) sums every column's gradient
+    serially (bit-identical to the reference even for hot columns: longer columns run as
+    serial chains beside the chunk pass, for every element type and gradient size);
     ``exact=False`` splits occurrence lists longer than ET_SGD_CHUNK (256) into partial
-    sums combined in a fixed order (deterministic).  The default (EXACT_DEFAULT = None) is
-    exact for Float32 tables — the chain path — and split for other dtypes, whose exact
-    mode has no fast path for hot columns.  Float16 tables
+    sums combined in a fixed order (deterministic, not the reference's order).  Float16 tables
     use Julia's Float16 arithmetic unless ``f16_fp32_acc`` (sums in Float32).
     ``hot_pass=True`` (experimental, ET_FLAG_SGD_HOT_PASS) sums the longest occurrence
     lists of Float32 dim-128 tables bag-major (deterministic, not bit-identical to the
@@ -412,20 +410,24 @@ def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool | 
     groups: dict = {}
     gsnap: dict = {}
     # indexers[i]: a snapshot of grads[i].indices, written by the update's index phase
-    snaps = {}
+    # (by position: one Indexer object may appear at several positions — the reference's
+    # sequential index!(indexers[i], ...) leaves it holding the LAST table's indices, so only
+    # its last position gets a snapshot; the others pass none)
+    snaps = [None] * len(grads)
     if indexers is not None:
-        for ix, A, g in zip(indexers, tables, grads):
-            if isinstance(ix, Indexer):
+        last = {id(ix): i for i, ix in enumerate(indexers) if isinstance(ix, Indexer)}
+        for i, (ix, A, g) in enumerate(zip(indexers, tables, grads)):
+            if isinstance(ix, Indexer) and last[id(ix)] == i:
                 if g.indices.numel() > 0:
-                    snaps[id(g)] = ix._defer(g.indices, A.size()[1])
+                    snaps[i] = ix._defer(g.indices, A.size()[1])
                 else:  # nothing to copy: the Indexer of an empty index array
                     ix._pending = (g.indices, int(A.size()[1]))
-    for A, g in zip(tables, grads):
+    for i, (A, g) in enumerate(zip(tables, grads)):
         if g.indices.numel() == 0:
             continue
         key = (fused_update_path(A), A.dtype)
         groups.setdefault(key, []).append(_update_desc(A, g))
-        sn = snaps.get(id(g))
+        sn = snaps[i]
         gsnap.setdefault(key, []).append(sn.data_ptr() if sn is not None else None)
     calls = []
     if groups:

@@ -25,7 +25,7 @@ const libhip = "libamdhip64.so"
 const ET_F32, ET_F16, ET_F64, ET_I32, ET_I64 = Cint(0), Cint(1), Cint(2), Cint(3), Cint(4)
 const ET_FLAG_NONTEMPORAL = UInt32(1)
 const ET_FLAG_EXACT_UPDATE = UInt32(4)      # every column summed serially (bit-identical)
-const ET_FLAG_EXACT_IF_FAST = UInt32(256)   # exact where the chain path runs (Float32), else split
+const ET_FLAG_EXACT_IF_FAST = UInt32(256)   # the default: exact (ABI v9: every eltype and size)
 const ET_FLAG_SGD_UNFUSED = UInt32(8)
 const ET_FLAG_SGD_F64_ALPHA = UInt32(16)
 const ET_FLAG_SGD_INDEX_ONLY = UInt32(32)   # phase 1 of update!: index all (src/sparseupdate.jl:210-213)
@@ -259,6 +259,21 @@ function lookup!(dst, A::Union{HipSplitEmbedding{S,T},DeviceColumns{S,T}},
     return dst
 end
 
+# The per-XCD work queues' block for et_maplookup_prealloc_q (ET_LOOKUP_QUEUE_BYTES, zeroed
+# once; every launch leaves it zero): one block serves every call, since every call of this
+# layer is ordered on the one stream().
+const ET_LOOKUP_QUEUE_BYTES = 128
+const QUEUE = Ref{Any}(nothing)
+function _queue_block()
+    if QUEUE[] === nothing
+        q = HipArray{UInt8}(undef, ET_LOOKUP_QUEUE_BYTES)
+        ccall((:hipMemset, libhip), Cint, (Ptr{Cvoid}, Cint, Csize_t), q.ptr, 0,
+              ET_LOOKUP_QUEUE_BYTES) == 0 || error("hipMemset failed")
+        QUEUE[] = q
+    end
+    return QUEUE[].ptr
+end
+
 # dst may have another float eltype U than the tables (PreallocationStrategy{U},
 # src/lookup.jl:284-315): then the _to entry converts on the store.
 function maplookup!(strategy::PreallocationStrategy, dst::HipMatrix{U},
@@ -272,11 +287,19 @@ function maplookup!(strategy::PreallocationStrategy, dst::HipMatrix{U},
         descs[t] = LookupDesc(tp, ldt, size(A, 2), size(A, 1), pool, pointer(i), pool, off, cpp)
         off += size(A, 1)
     end
-    check(ccall((:et_maplookup_prealloc_to, libembtab), Cint,
-                (Cint, Cint, Ptr{LookupDesc}, Int32, Int64, Ptr{Cvoid}, Int64, UInt32,
-                 Ptr{Cvoid}),
-                et_dtype(T), et_dtype(U), descs, length(descs), EmbeddingTables._batchsize(I),
-                dst.ptr, leading(dst), ET_FLAG_NONTEMPORAL, stream()))
+    if U === T
+        check(ccall((:et_maplookup_prealloc_q, libembtab), Cint,
+                    (Cint, Ptr{LookupDesc}, Int32, Int64, Ptr{Cvoid}, Int64, UInt32, Ptr{Cvoid},
+                     Ptr{Cvoid}),
+                    et_dtype(T), descs, length(descs), EmbeddingTables._batchsize(I), dst.ptr,
+                    leading(dst), ET_FLAG_NONTEMPORAL, _queue_block(), stream()))
+    else
+        check(ccall((:et_maplookup_prealloc_to, libembtab), Cint,
+                    (Cint, Cint, Ptr{LookupDesc}, Int32, Int64, Ptr{Cvoid}, Int64, UInt32,
+                     Ptr{Cvoid}),
+                    et_dtype(T), et_dtype(U), descs, length(descs), EmbeddingTables._batchsize(I),
+                    dst.ptr, leading(dst), ET_FLAG_NONTEMPORAL, stream()))
+    end
     return dst
 end
 
@@ -334,12 +357,11 @@ function _sparse_sgd(::Type{T}, descs::Vector{UpdateDesc}, eta::Float64, flags::
                 et_dtype(T), descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
 end
 
-# The exact update (ET_FLAG_EXACT_UPDATE, every column's gradient summed serially in the
-# reference's order) is the default wherever it has its fast serial-chain path: the default
-# `nothing` passes ET_FLAG_EXACT_IF_FAST (exact for Float32 tables, the split mode for
-# Float64 / Float16, whose exact mode sums a hot column in one wave); exact = true forces
-# it for every eltype, exact = false selects the split mode (long columns summed as
-# ordered partial sums: deterministic, not bit-identical).
+# The exact update (every column's gradient summed serially in the reference's order) is
+# the default: `nothing` passes ET_FLAG_EXACT_IF_FAST, exact for every eltype and gradient
+# size since ABI v9 (the serial-chain path); exact = true is the same, exact = false selects
+# the split mode (long columns summed as ordered partial sums: deterministic, not
+# bit-identical).
 const EXACT = Ref{Union{Nothing,Bool}}(nothing)
 _exact_flag(exact) = exact === nothing ? ET_FLAG_EXACT_IF_FAST :
                      exact ? ET_FLAG_EXACT_UPDATE : UInt32(0)

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define ET_ABI_VERSION 8
+#define ET_ABI_VERSION 9
 
 /* Status codes. */
 #define ET_OK 0
@@ -88,12 +88,11 @@ extern "C" {
                                     bag-major over 1024-bag windows instead of by per-
                                     occurrence gathers (deterministic; EXPERIMENTAL, slower
                                     today — DESIGN.md §7) */
-#define ET_FLAG_EXACT_IF_FAST 256u /* sparse SGD (ABI v8): ET_FLAG_EXACT_UPDATE where the
-                                    exact mode has its fast serial-chain path (Float32 with
-                                    batch < 2^24, ld_delta < 2^22 and batch * ld_delta < 2^30
-                                    for every descriptor), the split mode otherwise (other
-                                    dtypes would sum a hot column in one wave per column);
-                                    the bindings' default.  Ignored with ET_FLAG_EXACT_UPDATE */
+#define ET_FLAG_EXACT_IF_FAST 256u /* sparse SGD, the bindings' default: since ABI v9 the
+                                    same as ET_FLAG_EXACT_UPDATE — the exact mode's serial-
+                                    chain path covers every element type and gradient size
+                                    (ABI v8 resolved it to the split mode for non-Float32
+                                    tables and for batch * ld_delta >= 2^30) */
 
 /* Occurrences per chunk of the non-exact sparse SGD: a column with more occurrences than
  * this is summed as ordered partial sums of ET_SGD_CHUNK consecutive occurrences (so a
@@ -162,6 +161,19 @@ typedef struct et_lookup_desc {
 int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int32_t ntables,
                           int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                           void* stream);
+
+/* et_maplookup_prealloc with a caller-owned QUEUE BLOCK (ABI v9): `queue` is
+ * ET_LOOKUP_QUEUE_BYTES of 16-byte aligned device memory, ZERO before its first use; the
+ * multi-table launch then takes its work items from per-XCD queues in that block (an XCD
+ * that finishes its own items takes over another's, ~1% faster on BASELINE config 3) and
+ * leaves the block zero again when it completes.  A block may serve any number of calls
+ * that are ordered with each other (one stream, a captured and replayed HIP graph), never
+ * two calls that may run at the same time.  queue == NULL is et_maplookup_prealloc (the
+ * static XCD stripe schedule).  Results are identical either way. */
+#define ET_LOOKUP_QUEUE_BYTES 128
+int et_maplookup_prealloc_q(int dtype, const et_lookup_desc* descs, int32_t ntables,
+                            int64_t batch, void* dst, int64_t ld_dst, uint32_t flags, void* queue,
+                            void* stream);
 
 /* PreallocationStrategy{U} with a destination of another floating type than the
  * tables (src/lookup.jl:284-315: `similar(example(x), U, ...)`): every pooled sum is

@@ -37,7 +37,7 @@ def test_abi_version_and_last_error():
     from embtab import _lib
 
     L = _lib.load()
-    assert L.et_abi_version() == _lib.ET_ABI_VERSION == 8
+    assert L.et_abi_version() == _lib.ET_ABI_VERSION == 9
     assert isinstance(L.et_last_error(), bytes)
 
 

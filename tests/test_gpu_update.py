@@ -807,11 +807,10 @@ def test_update_workspace_at_any_alignment(shift):
 
 
 @pytest.mark.parametrize("kind", ["f32", "f64", "f16", "bf16"])
-def test_default_mode_is_exact_where_fast(oracle, kind):
-    """The default update (exact=None, ET_FLAG_EXACT_IF_FAST) is the exact mode for Float32
-    tables — the serial-chain path — and the split mode for the other dtypes, whose exact
-    mode would sum a hot column in one wave: the default's result equals
-    exact=True for f32 and exact=False otherwise, bit for bit."""
+def test_default_mode_is_exact_for_every_dtype(oracle, kind):
+    """The default update (exact=None, ET_FLAG_EXACT_IF_FAST) is the exact mode for every
+    dtype since ABI v9 (round 4: Float32 only, the split mode otherwise): the default's
+    result equals exact=True and the oracle's serial update bit for bit."""
     rng = np.random.default_rng(11)
     ncols, B, P, dim = 64, 512, 8, 64
     to = (lambda a: a.astype(np.float32)) if kind == "f32" else (lambda a: a)
@@ -827,9 +826,9 @@ def test_default_mode_is_exact_where_fast(oracle, kind):
                                      dev(delta) if dk == "f32" else _dev_typed(delta, dk), dev(I))
         et.update_(et.Descent(0.1), A, g, exact=mode)
         res[mode] = _host_bits(A.data)
-    want = res[True] if kind == "f32" else res[False]
-    assert bits_equal(res[None], want)
-    if kind == "f32":
-        ref = base.copy()
-        oracle.sgd(ref, delta, I, 0.1, fused=True)
-        assert bits_equal(res[None], ref)
+    assert bits_equal(res[None], res[True])
+    from embtab.tables import fused_update_path
+    ref = base.copy()
+    A = et.SimpleEmbedding(dev(base) if dk == "f32" else _dev_typed(base, dk), et.Static(dim))
+    oracle.sgd(ref, delta, I, 0.1, fused=fused_update_path(A), bf16=kind == "bf16")
+    assert bits_equal(res[None], ref.view(res[None].dtype))

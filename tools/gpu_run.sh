@@ -1,0 +1,86 @@
+#!/bin/bash
+# One parametrised GPU-box runner (replaces the round 1-4 one-off gpu_*.sh scripts).
+# Every step runs under its own time limit; the first failing step ends the call.
+#
+# Usage: tools/gpu_run.sh TAG STEP [STEP ...]      (outputs under gpurun_out/TAG/)
+#   tests            pytest -m gpu (all GPU tests)
+#   tests:EXPR       pytest -m gpu -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench            python bench.py (the driver's default run) -> bench.json
+#   trace            rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 3
+#   pmc              PMC traffic of the headline kernel (tools/pmc_traffic.sh, tools/traffic.py)
+#   exact            kernel trace of one exact config-4 update + its timeline
+#   upd:N            the config-4 update alone, N processes (tools/upd_only.py)
+#   ab:A:B:N         the config-4 update with library builds A and B (paths), alternating N times
+#   env:VAR=V,..:N   the config-4 update with the experiment build and env VAR=V (N times)
+#   py:SCRIPT[:ARGS] python3 tools/SCRIPT ARGS (ARGS: '+'-separated)
+set -o pipefail
+TAG=$1; shift
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+LIB=embeddingtables.jl_amd/embtab/libembtab_hip.so
+EXP=tools/alt/libembtab_hip_exp.so
+
+die() { echo "FAIL $1"; tail -25 "$2"; exit 1; }
+
+for step in "$@"; do
+  case "$step" in
+    tests)
+      timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1 || die tests "$OUT/pytest_gpu.log"
+      tail -1 "$OUT/pytest_gpu.log" ;;
+    tests:*)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        -k "${step#tests:}" > "$OUT/pytest_k.log" 2>&1 || die tests "$OUT/pytest_k.log"
+      tail -1 "$OUT/pytest_k.log" ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+        || die smoke "$OUT/smoke.log"
+      tail -1 "$OUT/smoke.log" ;;
+    bench)
+      timeout -k 10 500 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || die bench "$OUT/bench.err"
+      python3 -c "import json,sys; d=json.load(open('$OUT/bench.json')); c=d.get('config4_zipf_update',{}); \
+print('bench', round(d['ms_per_step'],4), 'ms frac', round(d['roofline']['frac'],4), 'upd', round(c.get('update_exact_ms',0),3), \
+'split', round(c.get('update_split_ms',0),3), 'fp16', round(d.get('config3_fp16',{}).get('julia_f16_arith',{}).get('kernel_ms',0),4), \
+'cfg2', d.get('config2_gather',{}).get('us_per_launch'))" ;;
+    trace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run --output-format csv \
+        -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 > "$OUT/bench_traced.json" \
+        2> "$OUT/bench_traced.err" || die trace "$OUT/bench_traced.err"
+      echo "trace ok" ;;
+    pmc)
+      bash tools/pmc_traffic.sh "$OUT/pmc" --steps 5 --warmup 1 --cpu-seconds 0 --no-extra || die pmc /dev/null
+      python3 tools/traffic.py "$OUT/pmc" k_pooled_vec criteo26_b65536 "$OUT/pmc/traffic.json" | tail -1 ;;
+    exact)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_exact" -o run --output-format csv \
+        -- python3 tools/exact_cfg4.py exact > "$OUT/exact_traced.txt" 2>&1 || die exact "$OUT/exact_traced.txt"
+      f=$(ls "$OUT"/prof_exact/*/run_kernel_trace.csv "$OUT"/prof_exact/run_kernel_trace.csv 2>/dev/null | head -1)
+      python3 tools/upd_timeline.py "$f" > "$OUT/exact_timeline.txt" && grep -E "chains|sgd_exact|total" "$OUT/exact_timeline.txt" ;;
+    upd:*)
+      for i in $(seq 1 "${step#upd:}"); do
+        timeout -k 10 200 python3 tools/upd_only.py > "$OUT/upd_$i.txt" 2>&1 || die upd "$OUT/upd_$i.txt"
+        echo "upd $(tail -1 "$OUT/upd_$i.txt")"
+      done ;;
+    ab:*)
+      IFS=: read -r _ A B N <<< "$step"
+      for i in $(seq 1 "${N:-2}"); do for v in A B; do
+        lib=$([ $v = A ] && echo "$A" || echo "$B")
+        ET_LIBRARY=$lib timeout -k 10 200 python3 tools/upd_only.py > "$OUT/ab_${v}_$i.txt" 2>&1 || die ab "$OUT/ab_${v}_$i.txt"
+        echo "$v=$lib $(tail -1 "$OUT/ab_${v}_$i.txt")"
+      done; done ;;
+    env:*)
+      IFS=: read -r _ SETS N <<< "$step"
+      for i in $(seq 1 "${N:-1}"); do
+        env ET_LIBRARY=$EXP $(echo "$SETS" | tr ',' ' ') timeout -k 10 200 python3 tools/upd_only.py \
+          > "$OUT/env_$i.txt" 2>&1 || die env "$OUT/env_$i.txt"
+        echo "$SETS $(tail -1 "$OUT/env_$i.txt")"
+      done ;;
+    py:*)
+      IFS=: read -r _ SCRIPT ARGS <<< "$step"
+      timeout -k 10 400 python3 "tools/$SCRIPT" $(echo "$ARGS" | tr '+' ' ') > "$OUT/${SCRIPT%.py}.txt" 2>&1 \
+        || die "$SCRIPT" "$OUT/${SCRIPT%.py}.txt"
+      tail -3 "$OUT/${SCRIPT%.py}.txt" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
