@@ -25,6 +25,7 @@
 // or  w = w - eta*acc  (unfused, the generic path; optionally evaluated in Float64 as
 // the reference's multi-table generic path does), chosen by ET_FLAG_SGD_UNFUSED /
 // ET_FLAG_SGD_F64_ALPHA.
+#include <algorithm>
 #include <mutex>
 
 #include "et_common.h"
@@ -2115,13 +2116,22 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
 // bound) take the leftover issue slots.
 constexpr uint32_t kChainReserveLds = 84 * 1024;  // > 80 KiB: one chain workgroup per CU
 
+#ifdef ET_EXPERIMENTS
+// Experiment builds: every chain item's start and end (s_memrealtime, 100 MHz), list, S,
+// 64-entry groups, item number and hardware id, read back by et_debug_chain_timeline
+// (tools/chain_timeline.py).
+constexpr uint32_t kCtlCap = 1u << 17;
+__device__ uint4 g_ctl[kCtlCap][2];
+__device__ uint32_t g_ctl_n;
+#endif
+
 template <typename T, typename C, int MODE, bool NT>
 __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
                                             uint32_t* __restrict__ counters,
                                             const ChainCol* __restrict__ chains,
                                             const uint32_t* __restrict__ order,
                                             const uint32_t* __restrict__ ent, int ns, C eta_c,
-                                            double eta64, uint32_t quad_min) {
+                                            double eta64, uint32_t quad_min, uint32_t list) {
     const int lane = threadIdx.x & 63;
     __builtin_amdgcn_s_setprio(3);
     const uint32_t items = counters[kCntM] * (uint32_t)ns * (uint32_t)kQuadItems;
@@ -2130,8 +2140,27 @@ __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
         if (lane == 0) it = atomicAdd(&counters[kCntNext], 1u);
         it = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)it, 0, 64));
         if (it >= items) break;
+#ifdef ET_EXPERIMENTS
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         sgd_chain_item<T, C, MODE, NT>(pack, ntables, chains, order, ent, ns, eta_c, eta64, it,
                                        quad_min);
+#ifdef ET_EXPERIMENTS
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const ChainCol c = chains[order[(it / (uint32_t)kQuadItems) / (uint32_t)ns]];
+        const bool ran = c.S != 0u && ((it % (uint32_t)kQuadItems) == 0u ||
+                                        (c.S == 1u && c.ngr >= quad_min));
+        if (lane == 0 && ran) {
+            const uint32_t k = atomicAdd(&g_ctl_n, 1u);
+            uint32_t hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            if (k < kCtlCap) {
+                g_ctl[k][0] = make_uint4((uint32_t)t0, (uint32_t)(t0 >> 32), (uint32_t)t1,
+                                         (uint32_t)(t1 >> 32));
+                g_ctl[k][1] = make_uint4(list << 24 | c.S, c.ngr, it, hw);
+            }
+        }
+#endif
     }
     __builtin_amdgcn_s_setprio(0);
 }
@@ -2140,9 +2169,10 @@ template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chains(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min) {
+    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
+    uint32_t list) {
     chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
-                                quad_min);
+                                quad_min, list);
 }
 
 // The same chain loop on SIMDs of its own: the kernel writes a255, so it is allocated the
@@ -2154,10 +2184,11 @@ template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chains_x(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min) {
+    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
+    uint32_t list) {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
     chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
-                                quad_min);
+                                quad_min, list);
 }
 
 // The rest of the update phase of an exact Float32 call in one launch: blocks [0, nch)
@@ -2583,7 +2614,7 @@ constexpr unsigned kExactGrid = 512;
 template <typename T, typename C, int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
                   const uint32_t* order, const uint32_t* ent, int ns, C eta_c, double eta64,
-                  unsigned nb, hipStream_t s, bool excl) {
+                  unsigned nb, hipStream_t s, bool excl, uint32_t list) {
     // the quad walk for Float32 S = 1 chains of at least this many 64-entry groups (§9 "The
     // quad walk": every S = 1 chain 5.56 ms, >= 4 K / 16 K / 64 K / 128 K entries 5.20 / 4.99 /
     // 4.07-4.16 / 4.36 ms, none 4.48-4.52; profiles/r03/c/ab_quad_min.txt)
@@ -2600,12 +2631,13 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
     if (excl) {
         hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT>), dim3(nb), dim3(256),
                            kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
-                           eta_c, eta64, quad_min);
+                           eta_c, eta64, quad_min, list);
         ET_LAUNCH_CHECK("k_sgd_chains_x");
         return ET_OK;
     }
     hipLaunchKernelGGL((k_sgd_chains<T, C, MODE, NT>), dim3(nb), dim3(256), kChainReserveLds, s,
-                       pack, ntables, counters, chains, order, ent, ns, eta_c, eta64, quad_min);
+                       pack, ntables, counters, chains, order, ent, ns, eta_c, eta64, quad_min,
+                       list);
     ET_LAUNCH_CHECK("k_sgd_chains");
     return ET_OK;
 }
@@ -2623,7 +2655,7 @@ int launch_chain_lists(const UpdatePack& pack, int ntables, UpdateWs& w, int ns,
         const unsigned eb = (unsigned)(cdiv64(items, 4) < wg ? cdiv64(items, 4) : wg);
         rc = launch_chains<T, C, MODE, NT>(pack, ntables, w.ec.counters, w.ec.chains, w.ec.order,
                                            w.ec.ent, ns, eta_c, eta64, eb, cr.ec_side,
-                                           (excl & 1u) != 0);
+                                           (excl & 1u) != 0, 0u);
         if (rc != ET_OK) return rc;
     }
     if (cr.eh_side) {
@@ -2632,13 +2664,13 @@ int launch_chain_lists(const UpdatePack& pack, int ntables, UpdateWs& w, int ns,
         const unsigned eb = (unsigned)(cdiv64(items, 4) < wg ? cdiv64(items, 4) : wg);
         rc = launch_chains<T, C, MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
                                            w.eh.ent, ns, eta_c, eta64, eb, cr.eh_side,
-                                           (excl & 4u) != 0);
+                                           (excl & 4u) != 0, 2u);
         if (rc != ET_OK) return rc;
     }
     return launch_chains<T, C, MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
                                          w.chain_ent, ns, eta_c, eta64,
                                          (unsigned)ET_KNOB("ET_CHAIN_WG", kRegWg), cr.side,
-                                         (excl & 2u) != 0);
+                                         (excl & 2u) != 0, 1u);
 }
 
 // The update phase of an exact Float32 call: the chain lists on the side streams, the chunk
@@ -3525,3 +3557,22 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
 }
 
 ET_OOB_READER(update)
+
+#ifdef ET_EXPERIMENTS
+// Experiment builds only: copy (and reset) the chain-item timeline, 2 x uint4 per item
+// (et_update.hip chain_items); *n = items recorded (may exceed cap).
+extern "C" int et_debug_chain_timeline(void* host, int64_t cap, int64_t* n) {
+    uint32_t k = 0, zero = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(&k, HIP_SYMBOL(et::g_ctl_n), 4, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    const int64_t m = std::min<int64_t>(std::min<int64_t>(k, cap), et::kCtlCap);
+    if (m > 0 && hipMemcpyFromSymbol(host, HIP_SYMBOL(et::g_ctl), (size_t)m * 32, 0,
+                                     hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(et::g_ctl_n), &zero, 4, 0, hipMemcpyHostToDevice) != hipSuccess)
+        return -1;
+    *n = k;
+    return 0;
+}
+#endif

@@ -13,14 +13,16 @@
 #   upd:N            the config-4 update alone, N processes (tools/upd_only.py)
 #   ab:A:B:N         the config-4 update with library builds A and B (paths), alternating N times
 #   env:VAR=V,..:N   the config-4 update with the experiment build and env VAR=V (N times)
+#   capture:M1,M2..  the update after each tools/capture_effect.py mode (none, capture, dummyN ...)
 #   py:SCRIPT[:ARGS] python3 tools/SCRIPT ARGS (ARGS: '+'-separated)
+#   exppy:SCRIPT[:ARGS]  the same with the experiment build (tools/exp_build.sh)
 set -o pipefail
 TAG=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 LIB=embeddingtables.jl_amd/embtab/libembtab_hip.so
-EXP=tools/alt/libembtab_hip_exp.so
+EXP=tools/exp/libembtab_hip_exp.so
 
 die() { echo "FAIL $1"; tail -25 "$2"; exit 1; }
 
@@ -76,10 +78,17 @@ print('bench', round(d['ms_per_step'],4), 'ms frac', round(d['roofline']['frac']
           > "$OUT/env_$i.txt" 2>&1 || die env "$OUT/env_$i.txt"
         echo "$SETS $(tail -1 "$OUT/env_$i.txt")"
       done ;;
-    py:*)
-      IFS=: read -r _ SCRIPT ARGS <<< "$step"
-      timeout -k 10 400 python3 "tools/$SCRIPT" $(echo "$ARGS" | tr '+' ' ') > "$OUT/${SCRIPT%.py}.txt" 2>&1 \
-        || die "$SCRIPT" "$OUT/${SCRIPT%.py}.txt"
+    capture:*)
+      for m in $(echo "${step#capture:}" | tr ',' ' '); do
+        timeout -k 10 240 python3 tools/capture_effect.py "$m" 10 >> "$OUT/capture_modes.jsonl" 2> "$OUT/capture_$m.err" \
+          || die "capture $m" "$OUT/capture_$m.err"
+        tail -1 "$OUT/capture_modes.jsonl"
+      done ;;
+    py:*|exppy:*)
+      IFS=: read -r KIND SCRIPT ARGS <<< "$step"
+      LIBV=$([ "$KIND" = exppy ] && echo "$EXP" || echo "")
+      ET_LIBRARY=$LIBV timeout -k 10 400 python3 "tools/$SCRIPT" $(echo "$ARGS" | tr '+' ' ') \
+        > "$OUT/${SCRIPT%.py}.txt" 2>&1 || die "$SCRIPT" "$OUT/${SCRIPT%.py}.txt"
       tail -3 "$OUT/${SCRIPT%.py}.txt" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
