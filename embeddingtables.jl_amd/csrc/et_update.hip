@@ -26,6 +26,7 @@
 // the reference's multi-table generic path does), chosen by ET_FLAG_SGD_UNFUSED /
 // ET_FLAG_SGD_F64_ALPHA.
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 
 #include "et_common.h"
@@ -1217,9 +1218,10 @@ __device__ __forceinline__ ChainTile chain_tile(const UpdatePack& pack, int ntab
     return c;
 }
 
-// Inclusive scan of one value per thread over a 1024-thread workgroup.
-__device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32_t* lds16,
-                                                              uint32_t* total) {
+// Inclusive scan of one value per thread over a workgroup of NW waves.
+template <int NW = 16>
+__device__ __forceinline__ uint32_t block_inclusive_scan(uint32_t v, uint32_t* lds16,
+                                                         uint32_t* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1229,7 +1231,7 @@ __device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32
     if (lane == 63) lds16[wave] = v;
     __syncthreads();
     uint32_t off = 0, all = 0;
-    for (int w = 0; w < 16; ++w) {
+    for (int w = 0; w < NW; ++w) {
         off += w < wave ? lds16[w] : 0u;
         all += lds16[w];
     }
@@ -1237,6 +1239,13 @@ __device__ __forceinline__ uint32_t block_inclusive_scan_1024(uint32_t v, uint32
     __syncthreads();
     return v + off;
 }
+
+// The single-workgroup steps of the regular chains' plan run at 256 threads: they are
+// launched beside the chunk pass, whose persistent workgroups leave each CU a few wave slots
+// but never the 16 a 1024-thread workgroup needs — round 4's 1024-thread k_chain_tiles
+// waited 0.73 ms for a CU (profiles/r05/capture/timeline_none.txt) for a few microseconds
+// of work.
+constexpr int kPlanThreads = 256;
 
 // The early hot-column candidates of the big tables (ET_EH, see EcList below): kEhK
 // ascending columns per table, ~0 past the last; EhMap says which tables have a list and
@@ -1262,7 +1271,7 @@ __device__ __forceinline__ int eh_slot(const uint32_t* cand, uint32_t c) {
 // sentinel column, nor for the columns of early-chain tables, ec_mask, nor for the
 // early hot-column candidates, eh: those chains are planned from the index arrays, k_ec_*),
 // the first tile of each column, the tile -> column map and the tile total (counters[kCntT]).
-__global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntables,
+__global__ __launch_bounds__(kPlanThreads) void k_chain_tiles(UpdatePack pack, int ntables,
                                                       uint32_t ec_mask, EhMap eh,
                                                       const uint32_t* __restrict__ cand,
                                                       const uint32_t* __restrict__ keys,
@@ -1276,11 +1285,11 @@ __global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntabl
     const uint32_t M = counters[kCntM];
     if (eh.mask) {
         const int ne = __popc(eh.mask);
-        for (int i = threadIdx.x; i < ne * kEhK; i += 1024) sc[i] = cand[i];
+        for (int i = threadIdx.x; i < ne * kEhK; i += kPlanThreads) sc[i] = cand[i];
         __syncthreads();
     }
     uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < M; b0 += 1024) {
+    for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads) {
         const uint32_t m = b0 + threadIdx.x;
         uint32_t v = 0;
         if (m < M) {
@@ -1293,7 +1302,7 @@ __global__ __launch_bounds__(1024) void k_chain_tiles(UpdatePack pack, int ntabl
             v = early ? 0u : cdiv_u32(se - ss, kChainTile);
         }
         uint32_t total;
-        const uint32_t inc = block_inclusive_scan_1024(v, lds16, &total);
+        const uint32_t inc = block_inclusive_scan<kPlanThreads / 64>(v, lds16, &total);
         if (m < M) {
             const uint32_t t0 = carry + inc - v;
             tile0[m] = t0;
@@ -1393,7 +1402,7 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
 // the dispatch order: columns bucketed by log2 of their cost (entries x (S + overhead)),
 // costliest bucket first; the order inside a bucket is arbitrary (results never depend
 // on which wave takes a column).
-__global__ __launch_bounds__(1024) void k_chain_plan(const uint32_t* __restrict__ counters,
+__global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __restrict__ counters,
                                                      const uint32_t* __restrict__ cnt,
                                                      const uint2* __restrict__ info,
                                                      uint32_t* __restrict__ e0,
@@ -1409,11 +1418,11 @@ __global__ __launch_bounds__(1024) void k_chain_plan(const uint32_t* __restrict_
         return c ? (uint32_t)__clzll((long long)c) : 64u;
     };
     uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < M; b0 += 1024) {
+    for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads) {
         const uint32_t m = b0 + threadIdx.x;
         const uint32_t v = m < M ? cnt[m] : 0u;
         uint32_t total;
-        const uint32_t inc = block_inclusive_scan_1024(v, lds16, &total);
+        const uint32_t inc = block_inclusive_scan<kPlanThreads / 64>(v, lds16, &total);
         if (m < M) {
             e0[m] = carry + inc - v;
             atomicAdd(&hist[bucket(m)], 1u);
@@ -1430,7 +1439,7 @@ __global__ __launch_bounds__(1024) void k_chain_plan(const uint32_t* __restrict_
         }
     }
     __syncthreads();
-    for (uint32_t m = threadIdx.x; m < M; m += 1024) {
+    for (uint32_t m = threadIdx.x; m < M; m += kPlanThreads) {
         order[atomicAdd(&hist[bucket(m)], 1u)] = m;
     }
 }
@@ -2175,6 +2184,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                                 quad_min, list);
 }
 
+// Eight chain waves per workgroup (two per SIMD; one workgroup per CU by the LDS
+// reservation): for latency-bound lists (the early hot columns' S = 1 quad walks spend about a
+// third of their cycles issuing), so one CU keeps twice the gradient loads in flight.
+template <typename T, typename C, int MODE, bool NT>
+__global__ __launch_bounds__(512) void k_sgd_chains_w(
+    UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
+    const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
+    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
+    uint32_t list) {
+    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
+                                quad_min, list);
+}
+
 // The same chain loop on SIMDs of its own: the kernel writes a255, so it is allocated the
 // whole accumulation-register file besides its VGPRs and no other wave — of the chunk pass,
 // the singles, the index phase — can be resident on its SIMDs while it runs; the chain waves
@@ -2447,7 +2469,7 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
     const int64_t tmax = chain_tiles_max(n, chunk);
     const unsigned tg = (unsigned)(tmax < 8192 ? tmax : 8192);
-    hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(1024), 0, s, pack, ntables, ec_mask, eh,
+    hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(kPlanThreads), 0, s, pack, ntables, ec_mask, eh,
                        w.eh_cand, out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
                        w.chain_tile_col);
     hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
@@ -2456,7 +2478,7 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
                        w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
                        w.chain_info, w.chains, 4);
-    hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(1024), 0, s, w.counters, w.chain_cnt,
+    hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(kPlanThreads), 0, s, w.counters, w.chain_cnt,
                        w.chain_info, w.chain_e0, w.chain_order);
     hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                        out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
@@ -2614,7 +2636,7 @@ constexpr unsigned kExactGrid = 512;
 template <typename T, typename C, int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
                   const uint32_t* order, const uint32_t* ent, int ns, C eta_c, double eta64,
-                  unsigned nb, hipStream_t s, bool excl, uint32_t list) {
+                  unsigned nb, hipStream_t s, bool excl, uint32_t list, bool wide = false) {
     // the quad walk for Float32 S = 1 chains of at least this many 64-entry groups (§9 "The
     // quad walk": every S = 1 chain 5.56 ms, >= 4 K / 16 K / 64 K / 128 K entries 5.20 / 4.99 /
     // 4.07-4.16 / 4.36 ms, none 4.48-4.52; profiles/r03/c/ab_quad_min.txt)
@@ -2627,7 +2649,18 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
     ET_HIP_CHECK(attr_x);
+    static const hipError_t attr_w = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&k_sgd_chains_w<T, C, MODE, NT>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
+    ET_HIP_CHECK(attr_w);
     ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
+    if (wide) {
+        hipLaunchKernelGGL((k_sgd_chains_w<T, C, MODE, NT>), dim3(nb), dim3(512),
+                           kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
+                           eta_c, eta64, quad_min, list);
+        ET_LAUNCH_CHECK("k_sgd_chains_w");
+        return ET_OK;
+    }
     if (excl) {
         hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT>), dim3(nb), dim3(256),
                            kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
@@ -2662,9 +2695,11 @@ int launch_chain_lists(const UpdatePack& pack, int ntables, UpdateWs& w, int ns,
         const int64_t items = (int64_t)cr.eh_ncols * ns;
         const unsigned wg = (unsigned)ET_KNOB("ET_EH_WG", kEhWg);
         const unsigned eb = (unsigned)(cdiv64(items, 4) < wg ? cdiv64(items, 4) : wg);
+        // ET_EH_WIDE (experiments): eight waves per early-hot workgroup (k_sgd_chains_w)
+        const bool wide = ET_KNOB("ET_EH_WIDE", 0) != 0;
         rc = launch_chains<T, C, MODE, NT>(pack, ntables, w.eh.counters, w.eh.chains, w.eh.order,
                                            w.eh.ent, ns, eta_c, eta64, eb, cr.eh_side,
-                                           (excl & 4u) != 0, 2u);
+                                           (excl & 4u) != 0 && !wide, 2u, wide);
         if (rc != ET_OK) return rc;
     }
     return launch_chains<T, C, MODE, NT>(pack, ntables, w.counters, w.chains, w.chain_order,
@@ -2946,28 +2981,33 @@ inline EhMap eh_map(const EcList& eh) {
 // rest single chunks of the chunk pass.
 constexpr uint32_t kExactChunk = ET_SGD_CHUNK;
 
-// Four library streams per device (highest priority) carry ALL of an exact-mode call's
-// device work: stream 3 the index phase and the chunk pass (what a single-stream call runs
-// on the caller's stream), stream 0 the early chains, stream 2 the early hot columns (both
-// planned from the index arrays, forked at the start of the call), stream 1 the regular
-// chains (forked from stream 3 after the index phase).  The caller's stream only forks them
-// at the start and joins them at the end, inside the same library call, so a HIP graph
-// capture of the caller's stream captures every branch.  The fork/join events are shared,
-// so a call that uses the side streams holds `mu` from its first fork to its last join.
+// Three side streams per device (highest priority) for the exact mode's chains: stream 0
+// the early chains and stream 2 the early hot columns (both planned from the index arrays,
+// forked from the caller's stream at the start of the call), stream 1 the regular chains
+// (forked after the index phase); the index phase and the chunk pass run on the caller's
+// stream.  All are joined back into the caller's stream inside the same library call, so a
+// HIP graph capture of the caller's stream captures every branch.  The fork/join events are
+// shared, so a call that uses the side streams holds `mu` from its first fork to its last
+// join.
 //
-// Why the caller's stream carries no work: a process's hardware queues
-// share the command processor's pipes, and a queue whose chain launch is waiting for whole
-// CUs (one chain workgroup per CU, SIMDs of its own) holds up the dispatch of every other
-// queue on its pipe.  Round 4 ran the index phase on the caller's queue; whenever another
-// queue had been opened before the library's side streams (a torch.cuda.graph capture, or
-// ANY stream that had run a kernel — tools/capture_effect.py: dummy1..4, hidummy1,
-// capture), one side queue landed on the caller's pipe and the index phase's kernels ran
-// 2-4x longer (k_build_keys 174 -> 384 us, scans 5-14 -> 40-56 us; the update 4.07 ->
-// 5.15-5.34 ms; profiles/r05/capture_effect.txt).  With one side stream opened after the
-// library's, on a different pipe, nothing slowed (capture_after: 4.08 ms).  Now the four
-// streams that carry work are opened together, one after another (init() touches each
-// with an event record, which acquires its hardware queue), so they take consecutive
-// queues, and the caller's queue idles during the call.
+// When the side queues are opened matters.  A process's hardware queues
+// are spread over the command processor's pipes in the order they are opened (queue i on
+// pipe (i - 1) mod 4 fits every measurement below), and a queue that shares a pipe with a
+// queue holding a long-running kernel or a blocked barrier (a stream wait) dispatches its
+// own kernels 2-4x more slowly.  Round 4 opened the side queues at the first exact update:
+// the caller's queue is usually the process's first, so the three side queues took the three
+// other pipes — unless the process had opened other queues in between (a torch.cuda.graph
+// capture, or ANY stream that ran a kernel: tools/capture_effect.py), which put one side
+// queue on the caller's pipe: the index phase's kernels ran 2-4x longer and the config-4
+// update took 5.1-5.3 ms instead of 4.03-4.07 (profiles/r05/capture/).  Moving all of the
+// call's work to library streams (the caller's queue then holds only the join barriers) was
+// tried: 4.15-4.29 ms with other queues open, 4.63-4.69 ms without (the work queue then
+// shares the caller's pipe and its blocked join barrier; ET_WORK_STREAM=1 in experiment
+// builds, profiles/r05/queue_layout.txt).  So the caller's stream keeps the work, and the
+// side queues are opened at the FIRST call into the library on the device, of any entry
+// point (et::open_side_streams(), from every stream-taking ABI function), right after the
+// caller's own queue, before most programs open other streams; init() touches each with an
+// event record, which acquires its hardware queue.
 struct SideStreams {
     static constexpr int kN = 4;  // early chains, regular chains, early hot columns, work
     static constexpr int kEc = 0, kReg = 1, kEh = 2, kWork = 3;
@@ -2977,6 +3017,9 @@ struct SideStreams {
     hipEvent_t join[kN] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t cand = nullptr;  // the hot-column candidates are picked (k_eh_pick)
 };
+
+// The work stream (kWork) exists only for the ET_WORK_STREAM experiment.
+inline int side_stream_count() { return ET_KNOB("ET_WORK_STREAM", 0) ? 4 : 3; }
 
 inline SideStreams* side_streams() {
     static SideStreams streams[64];
@@ -2988,15 +3031,16 @@ inline SideStreams* side_streams() {
     if (!ss.cand) {
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
-        for (int i = 0; i < SideStreams::kN; ++i)
+        const int n = side_stream_count();
+        for (int i = 0; i < n; ++i)
             if ((!ss.fork[i] && hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming)) ||
                 (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
                 (!ss.st[i] &&
                  hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking, greatest)))
                 return nullptr;
-        // acquire the four hardware queues back to back (an event record is a packet on
-        // the stream's queue), so they are consecutive whatever the process opened before
-        for (int i = 0; i < SideStreams::kN; ++i)
+        // acquire the hardware queues now, back to back (an event record is a packet on the
+        // stream's queue)
+        for (int i = 0; i < n; ++i)
             if (hipEventRecord(ss.join[i], ss.st[i]) != hipSuccess) return nullptr;
         if (hipEventCreateWithFlags(&ss.cand, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
@@ -3095,6 +3139,7 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
 extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
                              uint32_t flags, void* workspace, int64_t ws_bytes, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     return sparse_sgd(dtype, descs, ntables, eta, flags, nullptr, workspace, ws_bytes, stream);
 }
 
@@ -3102,6 +3147,7 @@ extern "C" int et_sparse_sgd_snap(int dtype, const et_update_desc* descs, int32_
                                   double eta, uint32_t flags, int64_t* const* snaps,
                                   void* workspace, int64_t ws_bytes, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (!snaps) return et::fail(ET_ERR_ARG, "snaps is NULL");
     if (ntables > ET_MAX_TABLES_PER_LAUNCH)
         return et::fail(ET_ERR_ARG, "et_sparse_sgd_snap: at most %d tables per call",
@@ -3210,7 +3256,8 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     et::SideStreams* sides = chain ? et::side_streams() : nullptr;
     if (chain && !sides) return et::fail(ET_ERR_HIP, "sparse SGD: side streams unavailable");
     et::SideFork fork(sides, s);
-    if (chain) {  // the call's main-line work moves to the library's work stream
+    // ET_WORK_STREAM=1 (experiment builds): the main-line work on a library stream
+    if (chain && ET_KNOB("ET_WORK_STREAM", 0)) {
         s = fork.fork(et::SideStreams::kWork);
         if (!s) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
     }
@@ -3404,6 +3451,7 @@ extern "C" int et_index_build(const int64_t* idx, int32_t pool, int64_t ld_idx, 
                               int64_t* map, int64_t* nunique_dev, void* workspace,
                               int64_t ws_bytes, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (pool < 0 || batch < 0 || nrows < 0) return et::fail(ET_ERR_ARG, "negative size");
     const int64_t n = (int64_t)pool * batch;
     if (n >= 0x7fffffffll) return et::fail(ET_ERR_ARG, "too many occurrences");
@@ -3530,6 +3578,7 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
                                  int64_t ubegin, int64_t uend, const int64_t* map, double eta,
                                  uint32_t flags, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (dtype != ET_F32 && dtype != ET_F64 && dtype != ET_F16 && dtype != ET_BF16)
         return et::fail(ET_ERR_UNSUPPORTED, "update: dtype %d", dtype);
     if (uend <= ubegin || dim == 0) return ET_OK;
@@ -3557,6 +3606,20 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
 }
 
 ET_OOB_READER(update)
+
+namespace et {
+// Open this device's side queues at the first library call (see SideStreams); a no-op after
+// that, and while the caller's stream is capturing a graph.
+void open_side_streams(hipStream_t caller) {
+    static std::atomic<uint64_t> done{0};  // bit d: device d's side streams are open
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+    if (done.load(std::memory_order_relaxed) & (1ull << dev)) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(caller, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    if (side_streams()) done.fetch_or(1ull << dev);
+}
+}  // namespace et
 
 #ifdef ET_EXPERIMENTS
 // Experiment builds only: copy (and reset) the chain-item timeline, 2 x uint4 per item

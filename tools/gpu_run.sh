@@ -14,6 +14,7 @@
 #   ab:A:B:N         the config-4 update with library builds A and B (paths), alternating N times
 #   env:VAR=V,..:N   the config-4 update with the experiment build and env VAR=V (N times)
 #   capture:M1,M2..  the update after each tools/capture_effect.py mode (none, capture, dummyN ...)
+#   expcapture:VAR=V,..:M1,M2..  the same with the experiment build and env VAR=V
 #   py:SCRIPT[:ARGS] python3 tools/SCRIPT ARGS (ARGS: '+'-separated)
 #   exppy:SCRIPT[:ARGS]  the same with the experiment build (tools/exp_build.sh)
 set -o pipefail
@@ -83,6 +84,13 @@ print('bench', round(d['ms_per_step'],4), 'ms frac', round(d['roofline']['frac']
         timeout -k 10 240 python3 tools/capture_effect.py "$m" 10 >> "$OUT/capture_modes.jsonl" 2> "$OUT/capture_$m.err" \
           || die "capture $m" "$OUT/capture_$m.err"
         tail -1 "$OUT/capture_modes.jsonl"
+      done ;;
+    expcapture:*)
+      IFS=: read -r _ SETS MODES <<< "$step"
+      for m in $(echo "$MODES" | tr ',' ' '); do
+        env ET_LIBRARY=$EXP $(echo "$SETS" | tr ',' ' ') timeout -k 10 240 python3 tools/capture_effect.py "$m" 10 \
+          > "$OUT/expcap.tmp" 2> "$OUT/expcap_$m.err" || die "expcapture $m" "$OUT/expcap_$m.err"
+        echo "$SETS $(tail -1 "$OUT/expcap.tmp")" | tee -a "$OUT/expcapture.txt"
       done ;;
     py:*|exppy:*)
       IFS=: read -r KIND SCRIPT ARGS <<< "$step"
