@@ -608,6 +608,19 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
     if constexpr (D == 128 && sizeof(T) == 4) {
         const uint32_t fg = e >> 16;
         if (fg != 0u) {  // a feature slice of a split table (build_stripe_map)
+            if constexpr (SG) {
+                // G = 2: 256-byte half rows through the scalar-addressed loop with 8-byte lanes
+                // (round 4's 256-byte row loop, run_bags_s BPL = 8): the table and output
+                // columns start fofs features on, the row stride is the table's
+                if (sm.fsplit_g == 2) {
+                    et_lookup_desc h = pack.d[t];
+                    const int fofs = (int)(fg - 1u) * (D / 2);
+                    h.table = reinterpret_cast<const T*>(h.table) + fofs;
+                    h.dst_row_off += fofs;
+                    run_bags_s<T, A, U, NT, false, 8>(h, batch, dst, ld_dst, chunk, rounds);
+                    return;
+                }
+            }
             const int64_t per_round = SG ? 8 : 4 * VecGeom<T, D>::GPW;
             const int64_t b0 = chunk * per_round * rounds, b1 = b0 + per_round * rounds;
             const int fofs = (int)(fg - 1u) * (D / sm.fsplit_g);

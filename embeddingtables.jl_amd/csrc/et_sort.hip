@@ -21,6 +21,7 @@ constexpr int kScanThreads = 256;
 constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanThreads * kScanItems;  // 4096
 constexpr int kScanPartialsLds = 16384;               // partials staged in LDS (64 KB)
+constexpr int kScanStageMin = 1024;                   // fewer partials: read in place
 
 constexpr int kRsMaxBits = 9;  // digit width: 9 bits -> 3 passes for keys < 2^27
 constexpr int kRsMaxBuckets = 1 << kRsMaxBits;
@@ -80,7 +81,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t* __
     if (threadIdx.x == 0) part[blockIdx.x] = total;
 }
 
-// Exclusive scan of part[0..np) in place by one workgroup; part[np] = total.
+// Exclusive scan of part[0..np) in place by one workgroup; part[np] = total.  STAGED (host
+// chosen, np > kScanStageMin) stages the partials in 64 KB of LDS; the unstaged variant
+// asks for 16 bytes, so it finds a CU at once beside persistent workgroups that hold most
+// of the LDS (the exact update's chain-plan scan, 2-3 partials, waited 585 us for 64 KB
+// beside k_sgd_exact).
+template <bool STAGED>
 __global__ __launch_bounds__(kScanThreads) void k_scan_partials(uint32_t* __restrict__ part,
                                                                 int64_t np,
                                                                 const uint32_t* __restrict__ mlen,
@@ -95,8 +101,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_partials(uint32_t* __rest
     // 26 us for the 8.3 K tiles of a 34 M-key segment scan)
     // Up to 16384 partials (a 64 M-element scan) are staged in LDS with coalesced loads
     // and stores; the per-thread runs then read LDS instead of strided global words.
-    __shared__ uint32_t sp[kScanPartialsLds];
-    const bool staged = np <= kScanPartialsLds;  // workgroup-uniform
+    __shared__ uint32_t sp[STAGED ? kScanPartialsLds : 1];
+    const bool staged = STAGED && np <= kScanPartialsLds;  // workgroup-uniform
     uint32_t* p = staged ? sp : part;
     if (staged) {  // all loads issued before the LDS stores (one memory latency)
         uint32_t buf[kScanPartialsLds / kScanThreads];
@@ -174,6 +180,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const uint32_t* __re
     }
 }
 
+inline void launch_scan_partials(uint32_t* part, int64_t np, const uint32_t* mlen, uint32_t madd,
+                                 hipStream_t s) {
+    if (np > kScanStageMin)
+        hipLaunchKernelGGL(k_scan_partials<true>, dim3(1), dim3(kScanThreads), 0, s, part, np,
+                           mlen, madd);
+    else
+        hipLaunchKernelGGL(k_scan_partials<false>, dim3(1), dim3(kScanThreads), 0, s, part, np,
+                           mlen, madd);
+}
+
 // Exclusive scan of m (< 2^32 total) uint32 values; out may alias in.  out[m] is NOT
 // written; the total is left in part[np].  `part` needs cdiv(m, 4096) + 1 entries.
 // With `mlen`, only the first min(m, *mlen + madd) elements (a device-side length) are
@@ -186,7 +202,7 @@ inline int exclusive_scan_u32(const uint32_t* in, uint32_t* out, int64_t m, uint
     if (np > 0x7fffffffll) return fail(ET_ERR_ARG, "scan too large");
     hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, m, part,
                        mlen, madd);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, part, np, mlen, madd);
+    launch_scan_partials(part, np, mlen, madd, s);
     hipLaunchKernelGGL(k_scan_down, dim3((unsigned)np), dim3(kScanThreads), 0, s, in, out, m,
                        part, mlen, madd);
     ET_LAUNCH_CHECK("exclusive_scan_u32");

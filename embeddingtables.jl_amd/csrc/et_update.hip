@@ -1111,7 +1111,7 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
 // the reference: bit-identical, and no partial sums to combine.
 //
 // Index phase, over tiles of kChainTile occurrences so a 834,828-occurrence column is
-// cut by ~200 workgroups rather than walked by one wave: k_chain_tiles (tiles per
+// cut by ~200 workgroups rather than walked by one wave: k_chain_tile_count/_fill (tiles per
 // column), k_chain_tcount (per tile, the entries its runs make at each S), k_chain_choose
 // (per column, S and the entry count), k_chain_plan (entry offsets, columns ordered by
 // cost so the longest chains are dispatched first), k_chain_emit (the entries).  Update phase: the chain role of
@@ -1240,11 +1240,10 @@ __device__ __forceinline__ uint32_t block_inclusive_scan(uint32_t v, uint32_t* l
     return v + off;
 }
 
-// The single-workgroup steps of the regular chains' plan run at 256 threads: they are
-// launched beside the chunk pass, whose persistent workgroups leave each CU a few wave slots
-// but never the 16 a 1024-thread workgroup needs — round 4's 1024-thread k_chain_tiles
-// waited 0.73 ms for a CU (profiles/r05/capture/timeline_none.txt) for a few microseconds
-// of work.
+// The one-workgroup step of the regular chains' plan (k_chain_plan) runs at 256 threads: it
+// is launched beside the chunk pass, whose persistent workgroups leave each CU a few wave
+// slots but never the 16 a 1024-thread workgroup needs (round 4's 1024-thread tile pass waited
+// 0.73 ms for a CU, profiles/r05/capture/timeline_none.txt).
 constexpr int kPlanThreads = 256;
 
 // The early hot-column candidates of the big tables (ET_EH, see EcList below): kEhK
@@ -1267,30 +1266,27 @@ __device__ __forceinline__ int eh_slot(const uint32_t* cand, uint32_t c) {
     return lo < kEhK && cand[lo] == c ? lo : -1;
 }
 
-// Index phase 1 (one workgroup): tiles per chain column (none for the out-of-range
-// sentinel column, nor for the columns of early-chain tables, ec_mask, nor for the
-// early hot-column candidates, eh: those chains are planned from the index arrays, k_ec_*),
-// the first tile of each column, the tile -> column map and the tile total (counters[kCntT]).
-__global__ __launch_bounds__(kPlanThreads) void k_chain_tiles(UpdatePack pack, int ntables,
-                                                      uint32_t ec_mask, EhMap eh,
-                                                      const uint32_t* __restrict__ cand,
-                                                      const uint32_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ seg_start,
-                                                      const uint32_t* __restrict__ mlist,
-                                                      uint32_t* __restrict__ counters,
-                                                      uint32_t sent, uint32_t* __restrict__ tile0,
-                                                      uint32_t* __restrict__ tile_col) {
-    __shared__ uint32_t lds16[16];
+// Index phase 1a (grid): tiles per chain column into tile0[m] (none for the out-of-range
+// sentinel column, nor for the columns of early-chain tables, ec_mask, nor for the early
+// hot-column candidates, eh: those chains are planned from the index arrays, k_ec_*), and
+// tile0[M] = 0, ready for the exclusive scan that makes tile0 each column's first tile.
+__global__ __launch_bounds__(256) void k_chain_tile_count(UpdatePack pack, int ntables,
+                                                          uint32_t ec_mask, EhMap eh,
+                                                          const uint32_t* __restrict__ cand,
+                                                          const uint32_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ seg_start,
+                                                          const uint32_t* __restrict__ mlist,
+                                                          const uint32_t* __restrict__ counters,
+                                                          uint32_t sent,
+                                                          uint32_t* __restrict__ tile0) {
     __shared__ uint32_t sc[ET_MAX_TABLES_PER_LAUNCH * kEhK];  // the candidate lists
     const uint32_t M = counters[kCntM];
     if (eh.mask) {
         const int ne = __popc(eh.mask);
-        for (int i = threadIdx.x; i < ne * kEhK; i += kPlanThreads) sc[i] = cand[i];
+        for (int i = threadIdx.x; i < ne * kEhK; i += 256) sc[i] = cand[i];
         __syncthreads();
     }
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads) {
-        const uint32_t m = b0 + threadIdx.x;
+    for (uint32_t m = blockIdx.x * 256 + threadIdx.x; m <= M; m += gridDim.x * 256) {
         uint32_t v = 0;
         if (m < M) {
             const uint32_t u = mlist[m], ss = seg_start[u], se = seg_start[u + 1];
@@ -1301,16 +1297,21 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_tiles(UpdatePack pack, i
                                 eh_slot(sc + eh.e[t] * kEhK, k0 - pack.row_off[t]) >= 0);
             v = early ? 0u : cdiv_u32(se - ss, kChainTile);
         }
-        uint32_t total;
-        const uint32_t inc = block_inclusive_scan<kPlanThreads / 64>(v, lds16, &total);
-        if (m < M) {
-            const uint32_t t0 = carry + inc - v;
-            tile0[m] = t0;
-            for (uint32_t k = 0; k < v; ++k) tile_col[t0 + k] = m;
-        }
-        carry += total;
+        tile0[m] = v;
     }
-    if (threadIdx.x == 0) counters[kCntT] = carry;
+}
+
+// Index phase 1b (grid, after the exclusive scan of tile0): the tile -> column map and the
+// tile total (counters[kCntT] = tile0[M]).
+__global__ __launch_bounds__(256) void k_chain_tile_fill(const uint32_t* __restrict__ tile0,
+                                                         uint32_t* __restrict__ counters,
+                                                         uint32_t* __restrict__ tile_col) {
+    const uint32_t M = counters[kCntM];
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[kCntT] = tile0[M];
+    for (uint32_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
+        const uint32_t t0 = tile0[m], t1 = tile0[m + 1];
+        for (uint32_t k = t0; k < t1; ++k) tile_col[k] = m;
+    }
 }
 
 // Index phase 2: per tile, the entries its runs make at S = 1, 2, 4, 8, 16.
@@ -1572,7 +1573,7 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
 // bag with r > 0 — the same entries k_chain_emit would cut from the sorted list.  Which
 // columns are chains (more than `chunk` occurrences) is decided from the same counts
 // (occurrences in [1, nrows]), so the main index phase skips exactly these columns
-// (k_chain_tiles) and the chunk pass never sees them (they are multi-chunk).
+// (k_chain_tile_count) and the chunk pass never sees them (they are multi-chunk).
 constexpr int kEcMaxRows = 128;  // tables with at most this many rows
 constexpr int kEcBags = 256;     // bags per workgroup of k_ec_count / k_ec_emit
 constexpr int kEcMaxPool = 255;  // per-bag counts fit a byte
@@ -1587,7 +1588,7 @@ constexpr int kEcStats = 8;      // per (column, block): occurrences, entries at
 // the call instead of after the sort.  The slots are counted, planned and emitted by the
 // same k_ec_* kernels (a bag's indices are matched against the table's candidate list); a
 // candidate with more than `chunk` occurrences is a chain there, and the regular plan skips
-// it (k_chain_tiles), so every column is summed exactly once.
+// it (k_chain_tile_count), so every column is summed exactly once.
 constexpr int kEhSampleBags = 1024;     // bags sampled by k_eh_pick
 constexpr uint32_t kEhMinOcc = 32768;   // expected occurrences of a candidate (ET_EH_MIN)
 constexpr int kEhHash = 4096;           // LDS hash slots of the sample count
@@ -1911,7 +1912,13 @@ __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
 // 128 entries.  The 64-entry chunk is loaded permuted (lane 16r + k holds entry 4k + r),
 // so DPP row_newbcast:k hands row r entry 4k + r.  Same adds in the same order as the
 // 64-feature loop (bit-identical); rows 1-3 add garbage that is never stored.
-constexpr int kQuadRing = 32;   // quads (4 entries each) of gradient loads in flight
+// The ring holds R quads (R / 16 chunks): 32 (128 entries in flight) in the regular list,
+// whose waves share SIMDs with the chunk pass at 5 waves per SIMD (~100 VGPRs each), 64 (256
+// entries, 64 ring VGPRs) on the exclusive SIMDs of k_sgd_chains_x, whose waves have the
+// register file to themselves: the hot columns' walks are latency-bound, so twice the loads
+// in flight is twice the entries per microsecond until issue binds (~11 cycles per entry).
+constexpr int kQuadRing = 32;   // quads (4 entries each) of gradient loads in flight (default)
+constexpr int kQuadRingX = 64;  // the same on exclusive SIMDs (k_sgd_chains_x)
 constexpr int kQuadItems = 4;   // work items per (column, 64-feature slice): 16-feature quarters
 constexpr int kQuadMinGroups = 1024;  // quad walk for S = 1 chains of >= 64 K entries
 
@@ -1920,10 +1927,12 @@ __device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + K, 0xf, 0xf, false);
 }
 
-template <int J, int N>
-__device__ __forceinline__ void quad_trip(float (&x)[kQuadRing], float& acc, uint32_t cnext0,
-                                          uint32_t cnext1, __amdgpu_buffer_rsrc_t rx,
-                                          uint32_t ld4, uint32_t lane4) {
+// Quads x[J], J in [J, N) (one half-trip, 32 quads, 128 entries), then their reloads: quad
+// q + R into x[J], its bag from the chunk pair (cn0, cn1) R / 16 chunks on.
+template <int R, int J, int N>
+__device__ __forceinline__ void quad_trip(float (&x)[R], float& acc, uint32_t cn0, uint32_t cn1,
+                                          __amdgpu_buffer_rsrc_t rx, uint32_t ld4,
+                                          uint32_t lane4) {
     if constexpr (J < N) {
         const uint32_t v = __float_as_uint(x[J]);
         acc = acc + x[J];                                            // entry 4q
@@ -1934,35 +1943,39 @@ __device__ __forceinline__ void quad_trip(float (&x)[kQuadRing], float& acc, uin
         acc = acc + __uint_as_float(z);                              // entry 4q + 2
         const auto t16 = __builtin_amdgcn_permlane16_swap(z, z, false, false);
         acc = acc + __uint_as_float(t16[1]);                         // entry 4q + 3
-        // quad q + kQuadRing into x[J] (its bag from the chunk two chunks on)
-        const uint32_t bag = row_bcast<J & 15>(J < 16 ? cnext0 : cnext1);
+        const uint32_t bag = row_bcast<J & 15>((J & 31) < 16 ? cn0 : cn1);
         x[J] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             rx, (int)(__umul24(bag, ld4) + lane4), 0, 0));
-        quad_trip<J + 1, N>(x, acc, cnext0, cnext1, rx, ld4, lane4);
+        quad_trip<R, J + 1, N>(x, acc, cn0, cn1, rx, ld4, lane4);
     }
 }
 
-template <int J, int N>
-__device__ __forceinline__ void quad_prologue(float (&x)[kQuadRing], uint32_t c0, uint32_t c1,
+// Quads 0..R-1: x[J] from chunk J / 16 (c[0..R/16)).
+template <int R, int J>
+__device__ __forceinline__ void quad_prologue(float (&x)[R], const uint32_t (&c)[R / 16],
                                               __amdgpu_buffer_rsrc_t rx, uint32_t ld4,
                                               uint32_t lane4) {
-    if constexpr (J < N) {
-        const uint32_t bag = row_bcast<J & 15>(J < 16 ? c0 : c1);
+    if constexpr (J < R) {
+        const uint32_t bag = row_bcast<J & 15>(c[J / 16]);
         x[J] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
             rx, (int)(__umul24(bag, ld4) + lane4), 0, 0));
-        quad_prologue<J + 1, N>(x, c0, c1, rx, ld4, lane4);
+        quad_prologue<R, J + 1>(x, c, rx, ld4, lane4);
     }
 }
 
-// The serial sum of one S = 1 chain over 16 features (row 0 of the result).  ent: the
-// chain's entries (ngr x 64, then >= kChainPad padding entries that address bag `batch`,
-// past the gradient's range: they load +0); P: entries readable (range of the entry loads,
-// past it they read 0).  Trips of 2 chunks (32 quads); the last trip's adds reach at most
-// 64 entries past ngr x 64, inside the padding.
+// The serial sum of one S = 1 chain over 16 features (row 0 of the result), R quads of
+// gradient loads in flight.  ent: the chain's entries (ngr x 64, then >= kChainPad padding
+// entries that address bag `batch`, past the gradient's range: they load +0); P: entries
+// readable (range of the entry loads, past it they read 0, i.e. bag 0: loaded into the ring
+// but never added).  Half-trips of 2 chunks (32 quads, 128 entries), alternating over the
+// ring's halves when R = 64; the last half-trip's adds reach at most 64 entries past
+// ngr x 64, inside the padding.
+template <int R>
 __device__ __forceinline__ float chain_walk_quad(const uint32_t* ent, uint32_t ngr, uint32_t P,
                                                  const float* delta, uint32_t range,
                                                  uint32_t lane4, uint32_t ld4) {
-    static_assert(kChainPad >= 64 && kQuadRing == 32, "quad walk layout");
+    static_assert(kChainPad >= 64 && (R == 32 || R == 64), "quad walk layout");
+    constexpr uint32_t RC = R / 16;  // chunks in the ring
     const int lane = threadIdx.x & 63;
     const uint32_t poff = 4u * (4u * (uint32_t)(lane & 15) + (uint32_t)(lane >> 4));
     const __amdgpu_buffer_rsrc_t rx =
@@ -1970,17 +1983,28 @@ __device__ __forceinline__ float chain_walk_quad(const uint32_t* ent, uint32_t n
     const __amdgpu_buffer_rsrc_t re =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(ent), 0, (int)(4u * P), 0x00020000);
     auto chunk = [&](uint32_t c) { return __builtin_amdgcn_raw_buffer_load_b32(re, (int)(c * 256u + poff), 0, 0); };
-    const uint32_t c0 = chunk(0), c1 = chunk(1);
-    uint32_t n0 = chunk(2), n1 = chunk(3);
-    float x[kQuadRing];
-    quad_prologue<0, kQuadRing>(x, c0, c1, rx, ld4, lane4);  // quads 0..31 (chunks 0, 1)
+    uint32_t c[RC];
+#pragma unroll
+    for (uint32_t k = 0; k < RC; ++k) c[k] = chunk(k);
+    uint32_t n0 = chunk(RC), n1 = chunk(RC + 1);  // the reloads of half-trip 0
+    float x[R];
+    quad_prologue<R, 0>(x, c, rx, ld4, lane4);  // quads 0..R-1
     float acc = 0.0f;
-    const uint32_t trips = (ngr + 1u) / 2u;
-    for (uint32_t t = 0; t < trips; ++t) {
-        const uint32_t m0 = chunk(2u * t + 4u), m1 = chunk(2u * t + 5u);
-        quad_trip<0, kQuadRing>(x, acc, n0, n1, rx, ld4, lane4);
-        n0 = m0;
-        n1 = m1;
+    const uint32_t nh = (ngr + 1u) / 2u;  // half-trips
+    for (uint32_t h = 0; h < nh; h += R / 32) {
+        {
+            const uint32_t m0 = chunk(2u * h + RC + 2u), m1 = chunk(2u * h + RC + 3u);
+            quad_trip<R, 0, 32>(x, acc, n0, n1, rx, ld4, lane4);
+            n0 = m0;
+            n1 = m1;
+        }
+        if constexpr (R == 64) {
+            if (h + 1u == nh) break;
+            const uint32_t m0 = chunk(2u * h + RC + 4u), m1 = chunk(2u * h + RC + 5u);
+            quad_trip<R, 32, 64>(x, acc, n0, n1, rx, ld4, lane4);
+            n0 = m0;
+            n1 = m1;
+        }
     }
     return acc;
 }
@@ -2041,7 +2065,7 @@ __device__ __forceinline__ C chain_walk_wide(const uint32_t* ent, uint32_t ngr, 
 // (the quad walk, 16 features each); any other chain takes the whole slice in quarter 0
 // (the other quarters return at once).  T is the table and gradient type, C the
 // accumulator (sgd_apply_t).
-template <typename T, typename C, int MODE, bool NT>
+template <typename T, typename C, int MODE, bool NT, int QR>
 __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntables,
                                                const ChainCol* __restrict__ chains,
                                                const uint32_t* __restrict__ order,
@@ -2077,7 +2101,7 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
             const int f = f0 + (lane & 15);
             const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
             const uint32_t ld = (uint32_t)d.ld_delta;
-            const float acc = chain_walk_quad(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
+            const float acc = chain_walk_quad<QR>(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
                                               (uint32_t)d.batch * ld * 4u, 4u * fc, 4u * ld);
             if (lane < 16 && f < d.dim) {
                 float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
@@ -2134,7 +2158,7 @@ __device__ uint4 g_ctl[kCtlCap][2];
 __device__ uint32_t g_ctl_n;
 #endif
 
-template <typename T, typename C, int MODE, bool NT>
+template <typename T, typename C, int MODE, bool NT, int QR = kQuadRing>
 __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
                                             uint32_t* __restrict__ counters,
                                             const ChainCol* __restrict__ chains,
@@ -2152,8 +2176,8 @@ __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
 #ifdef ET_EXPERIMENTS
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        sgd_chain_item<T, C, MODE, NT>(pack, ntables, chains, order, ent, ns, eta_c, eta64, it,
-                                       quad_min);
+        sgd_chain_item<T, C, MODE, NT, QR>(pack, ntables, chains, order, ent, ns, eta_c, eta64,
+                                           it, quad_min);
 #ifdef ET_EXPERIMENTS
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
         const ChainCol c = chains[order[(it / (uint32_t)kQuadItems) / (uint32_t)ns]];
@@ -2202,15 +2226,15 @@ __global__ __launch_bounds__(512) void k_sgd_chains_w(
 // the singles, the index phase — can be resident on its SIMDs while it runs; the chain waves
 // then issue at the SIMD's own rate instead of sharing it (the early chains and the early hot
 // columns by default, kChainExcl).
-template <typename T, typename C, int MODE, bool NT>
+template <typename T, typename C, int MODE, bool NT, int QR>
 __global__ __launch_bounds__(256) void k_sgd_chains_x(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
     const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
     uint32_t list) {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
-    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
-                                quad_min, list);
+    chain_items<T, C, MODE, NT, QR>(pack, ntables, counters, chains, order, ent, ns, eta_c,
+                                    eta64, quad_min, list);
 }
 
 // The rest of the update phase of an exact Float32 call in one launch: blocks [0, nch)
@@ -2328,6 +2352,7 @@ struct UpdateWs {
     // the index phase's tiles: first tile per column, tile -> column, entries per tile at
     // S = 1..16
     uint32_t *chain_tile0, *chain_tile_col, *chain_tcnt;
+    uint32_t* chain_part;  // the regular plan's scan partials (its own: it runs beside others)
     // early chains (EcList): per (column, block) stats and entry offsets, per EC column the
     // padded entry count, (S, entries), descriptor and cost order, their entries, and a
     // counter block (kCntM = EC columns) for the chain role
@@ -2395,7 +2420,8 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
     w.chain_order = (uint32_t*)take(4 * mmax);
     w.chain_info = (uint2*)take(8 * mmax);
     const int64_t tmax = chain_tiles_max(n, chunk);
-    w.chain_tile0 = (uint32_t*)take(4 * mmax);
+    w.chain_tile0 = (uint32_t*)take(4 * (mmax + 1));
+    w.chain_part = (uint32_t*)take(4 * scan_part_entries(mmax + 1));
     w.chain_tile_col = (uint32_t*)take(4 * tmax);
     w.chain_tcnt = (uint32_t*)take(20 * tmax);
     auto carve_ec = [&](const EcList* l, int64_t occ) {
@@ -2468,9 +2494,21 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     const int64_t mmax = n / chunk + 2;
     const unsigned cg = (unsigned)(cdiv64(mmax, 4) < 2048 ? cdiv64(mmax, 4) : 2048);
     const int64_t tmax = chain_tiles_max(n, chunk);
-    const unsigned tg = (unsigned)(tmax < 8192 ? tmax : 8192);
-    hipLaunchKernelGGL(k_chain_tiles, dim3(1), dim3(kPlanThreads), 0, s, pack, ntables, ec_mask, eh,
-                       w.eh_cand, out.keys, w.seg_start, w.mlist, w.counters, sent, w.chain_tile0,
+    // grid-stride over the tiles (about 10 K on config 4): round 4's 8192 workgroups waited
+    // beside the chunk pass for slots (k_chain_tcount 127-507 us, k_chain_emit 323-351 us)
+    const long long tgmax = ET_KNOB("ET_PLAN_TG", 2048ll);
+    const unsigned tg = (unsigned)(tmax < tgmax ? tmax : tgmax);
+    // tiles per column, their exclusive scan (device-side length M + 1), the tile map: small
+    // grids that fit beside the chunk pass's persistent workgroups (round 4's one-workgroup
+    // k_chain_tiles serialised M / 1024 dependent scan rounds and waited up to 0.73 ms for a CU)
+    const unsigned mg = (unsigned)(cdiv64(mmax + 1, 256) < 256 ? cdiv64(mmax + 1, 256) : 256);
+    hipLaunchKernelGGL(k_chain_tile_count, dim3(mg), dim3(256), 0, s, pack, ntables, ec_mask, eh,
+                       w.eh_cand, out.keys, w.seg_start, w.mlist, w.counters, sent,
+                       w.chain_tile0);
+    int rc = exclusive_scan_u32(w.chain_tile0, w.chain_tile0, mmax + 1, w.chain_part, s,
+                                w.counters + kCntM, 1);
+    if (rc != ET_OK) return rc;
+    hipLaunchKernelGGL(k_chain_tile_fill, dim3(mg), dim3(256), 0, s, w.chain_tile0, w.counters,
                        w.chain_tile_col);
     hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                        out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
@@ -2538,8 +2576,7 @@ inline int group_occurrences(const UpdatePack& pack, int ntables, int64_t n, uin
         const int64_t np = cdiv64(n, kScanTile);
         hipLaunchKernelGGL(k_seg_reduce, dim3((unsigned)np), dim3(kScanThreads), 0, s, out.keys,
                            n, w.part);
-        hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kScanThreads), 0, s, w.part, np,
-                           nullptr, 0u);
+        launch_scan_partials(w.part, np, nullptr, 0u, s);
         hipLaunchKernelGGL(k_seg_down, dim3((unsigned)np), dim3(kScanThreads), 0, s, out.keys,
                            n, w.part, w.seg_start, w.counters);
         ET_LAUNCH_CHECK("k_seg_down");
@@ -2629,8 +2666,12 @@ constexpr unsigned kChainExcl = 5;
 // flight than the split mode's 16384 + 16384 leaves the fabric to the latency-bound chains
 // beside it (config 4, A/B twice on one box: 4.22-4.24 ms at the split mode's grid, 4.05-4.06
 // at 384-768, 4.20 at 256; the split mode itself is faster at its own grid, 3.00 vs 3.61 ms;
-// profiles/r04/ab_exact_grid.txt).
-constexpr unsigned kExactGrid = 512;
+// profiles/r04/ab_exact_grid.txt).  384, not 512: 2 x 384 workgroups fit at once beside the 64
+// CUs of exclusive early chains (4 per free CU, 1 per chain CU: 832), so none of them is left
+// pending in the dispatcher — a pending one held back every dispatch with LDS on the other
+// queues (the regular plan's k_scan_down, 17 KB, waited 0.6 ms; 4.01-4.02 ms at 384 against
+// 4.16 at 512, profiles/r05/exact_grid/).
+constexpr unsigned kExactGrid = 384;
 
 // k_sgd_chains on stream `s`: zero the item counter, at most `nb` workgroups.
 template <typename T, typename C, int MODE, bool NT>
@@ -2646,9 +2687,15 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
     ET_HIP_CHECK(attr);
     static const hipError_t attr_x = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT>),
+        reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT, kQuadRingX>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
     ET_HIP_CHECK(attr_x);
+#ifdef ET_EXPERIMENTS
+    static const hipError_t attr_x32 = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT, kQuadRing>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
+    ET_HIP_CHECK(attr_x32);
+#endif
     static const hipError_t attr_w = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&k_sgd_chains_w<T, C, MODE, NT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
@@ -2662,7 +2709,16 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         return ET_OK;
     }
     if (excl) {
-        hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT>), dim3(nb), dim3(256),
+#ifdef ET_EXPERIMENTS
+        if (ET_KNOB("ET_QUAD_RING_X", kQuadRingX) != kQuadRingX) {  // the 32-quad ring
+            hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT, kQuadRing>), dim3(nb), dim3(256),
+                               kChainReserveLds, s, pack, ntables, counters, chains, order, ent,
+                               ns, eta_c, eta64, quad_min, list);
+            ET_LAUNCH_CHECK("k_sgd_chains_x");
+            return ET_OK;
+        }
+#endif
+        hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT, kQuadRingX>), dim3(nb), dim3(256),
                            kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
                            eta_c, eta64, quad_min, list);
         ET_LAUNCH_CHECK("k_sgd_chains_x");
@@ -3079,7 +3135,7 @@ struct SideFork {
 
 // The early-chain plan (k_ec_count -> k_ec_plan -> k_ec_emit) on stream `s`; for the
 // hot-column list (ec.hot) after picking the candidates (k_eh_pick), whose completion
-// `cand_ready` records for the regular plan (k_chain_tiles skips the candidates).
+// `cand_ready` records for the regular plan (k_chain_tile_count skips the candidates).
 inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chunk,
                           const UpdateWs::EcWs& w, const uint32_t* cand_c, int ns, hipStream_t s,
                           hipEvent_t cand_ready = nullptr) {

@@ -5,13 +5,16 @@
 # (et_debug_chain_timeline).  Output: tools/exp/libembtab_hip_exp.so, loaded with
 #   ET_LIBRARY=tools/exp/libembtab_hip_exp.so ET_<KNOB>=<value> python ...
 # The package's own library (embtab/libembtab_hip.so) never reads the environment.
-# EXTRA_DEFINES="A B" adds -DA -DB.
+# EXTRA_DEFINES="A B" adds -DA -DB; EXP_NAME=x writes tools/exp/libembtab_hip_x.so instead
+# (objects under tools/exp/obj_x), so a variant build leaves the default experiment build alone.
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/exp
+NAME=${EXP_NAME:-exp}
+SUF=$([ "$NAME" = exp ] && echo "" || echo "_$NAME")
 python3 - <<PY
 import __graft_entry__ as g
 g.build_hip(defines=["ET_EXPERIMENTS"] + "${EXTRA_DEFINES:-}".split(),
-            lib="tools/exp/libembtab_hip_exp.so", obj_dir="tools/exp/obj")
+            lib="tools/exp/libembtab_hip_$NAME.so", obj_dir="tools/exp/obj$SUF")
 PY
-echo tools/exp/libembtab_hip_exp.so
+echo tools/exp/libembtab_hip_$NAME.so

@@ -10,6 +10,10 @@
 #   trace            rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 3
 #   pmc              PMC traffic of the headline kernel (tools/pmc_traffic.sh, tools/traffic.py)
 #   exact            kernel trace of one exact config-4 update + its timeline
+#   classpmc         PMC traffic + time of each headline table class alone (tools/class_pmc.py)
+#   lookab:LIB:S1;S2:N  the headline launch (kernel ms) with library LIB and env sets S1, S2
+#                    (VAR=V,VAR=V; NONE=0 for none), alternating N times
+#   expexact:VAR=V,..  the exact step with the experiment build and env VAR=V
 #   upd:N            the config-4 update alone, N processes (tools/upd_only.py)
 #   ab:A:B:N         the config-4 update with library builds A and B (paths), alternating N times
 #   env:VAR=V,..:N   the config-4 update with the experiment build and env VAR=V (N times)
@@ -60,6 +64,36 @@ print('bench', round(d['ms_per_step'],4), 'ms frac', round(d['roofline']['frac']
         -- python3 tools/exact_cfg4.py exact > "$OUT/exact_traced.txt" 2>&1 || die exact "$OUT/exact_traced.txt"
       f=$(ls "$OUT"/prof_exact/*/run_kernel_trace.csv "$OUT"/prof_exact/run_kernel_trace.csv 2>/dev/null | head -1)
       python3 tools/upd_timeline.py "$f" > "$OUT/exact_timeline.txt" && grep -E "chains|sgd_exact|total" "$OUT/exact_timeline.txt" ;;
+    classpmc)
+      for c in heavy mid light all; do
+        D=$OUT/classpmc/$c; mkdir -p "$D"
+        timeout -k 10 120 python3 tools/class_pmc.py $c 10 > "$D/time.json" 2> "$D/time.err" || die classpmc "$D/time.err"
+        for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+          tag=$(echo "$grp" | tr ' ' '_')
+          timeout -s KILL 100 rocprofv3 --pmc $grp -d "$D/$tag" -o run --output-format csv \
+            -- python3 tools/class_pmc.py $c 5 > "$D/$tag.log" 2>&1 || die "classpmc $c $tag" "$D/$tag.log"
+        done
+        python3 tools/traffic.py "$D" k_pooled_vec "class_$c" "$D/traffic.json" > /dev/null
+        python3 -c "import json; t=json.load(open('$D/time.json')); d=json.load(open('$D/traffic.json')); \
+print('$c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric', round(d.get('hbm_bytes_per_launch',0)/1e9,3), 'GB', \
+'compulsory', round(t['hbm_compulsory_bytes']/1e9,3), 'GB', 'alg', round(t['algorithmic_bytes']/1e9,3), 'GB', 'L2hit', round(d.get('l2_hit_rate',0),3))"
+      done ;;
+    lookab:*)
+      # the headline launch with experiment library A and env sets (VAR=V,...;VAR=V,...), N rounds
+      IFS=: read -r _ LIBV SETSALL N <<< "$step"
+      for i in $(seq 1 "${N:-2}"); do
+        for SETS in $(echo "$SETSALL" | tr ';' ' '); do
+          env ET_LIBRARY=$LIBV $(echo "$SETS" | tr ',' ' ') timeout -k 10 200 python3 bench.py --steps 40 --warmup 5 \
+            --cpu-seconds 0 --no-extra --no-check > "$OUT/lookab.json" 2> "$OUT/lookab.err" || die lookab "$OUT/lookab.err"
+          python3 -c "import json; d=json.load(open('$OUT/lookab.json')); print('$SETS', round(d['roofline']['kernel_ms'],4), round(d['roofline']['kernel_ms_median'],4))"
+        done
+      done ;;
+    expexact:*)
+      SETS=${step#expexact:}; T=$OUT/exp_$(echo "$SETS" | tr ',=' '__')
+      env ET_LIBRARY=$EXP $(echo "$SETS" | tr ',' ' ') timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+        -d "$T" -o run --output-format csv -- python3 tools/exact_cfg4.py exact > "$T.txt" 2>&1 || die expexact "$T.txt"
+      f=$(ls "$T"/*/run_kernel_trace.csv "$T"/run_kernel_trace.csv 2>/dev/null | head -1)
+      python3 tools/upd_timeline.py "$f" > "$T.timeline" && echo "$SETS" && grep -E "chains|sgd_exact|total" "$T.timeline" ;;
     upd:*)
       for i in $(seq 1 "${step#upd:}"); do
         timeout -k 10 200 python3 tools/upd_only.py > "$OUT/upd_$i.txt" 2>&1 || die upd "$OUT/upd_$i.txt"
