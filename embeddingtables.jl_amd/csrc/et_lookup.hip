@@ -830,6 +830,87 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
     }
 }
 
+// The same gather, software-pipelined over `rounds` rounds per workgroup: round r + 1's rows
+// are loaded before round r's are stored, and round r + 2's indices before those, so each
+// wave keeps a round of rows in flight while it writes the previous one.  The one-round
+// kernel loads every row of the launch, then stores them all: reads and writes never overlap
+// (config 2: 18.5 us per launch for 67.6 MB, compulsory traffic only, PMC
+// profiles/r05/cfg2/).  Vector memory counters retire in issue order, so the issue order is
+// indices(r + 2), store(r), rows(r + 1): the store waits only for round r's rows, the row
+// addresses of round r + 1 only for indices issued before them.  Rows of 16 * LPR bytes, one
+// vector per lane (NV = 1).  Bit copies, so any schedule gives the same bytes.
+template <int RB, bool NT>
+__global__ __launch_bounds__(256) void k_gather_pipe(LookupPack pack, int ntables, int64_t batch,
+                                                     char* __restrict__ dst, int64_t ld_dst_b,
+                                                     int es, int rounds) {
+    constexpr int VPR = RB / 16;
+    static_assert(VPR <= 64 && 64 % VPR == 0, "one vector per lane");
+    constexpr int LPR = VPR;
+    constexpr int GPW = 64 / LPR;
+    constexpr int U = 8;
+    const int64_t item = blockIdx.x;
+    const int t = (int)(item % ntables);
+    const int64_t chunk = item / ntables;
+    const et_lookup_desc& d = pack.d[t];
+    const char* table = reinterpret_cast<const char*>(d.table);
+    const int64_t ld_b = d.ld_table * es;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / LPR, sub = lane % LPR;
+    const int64_t per_round = 4 * GPW;
+    const int64_t step = per_round * U;  // bags per round
+    const int64_t bag_base = chunk * step * rounds + wave * GPW + g;
+    auto bag_of = [&](int r, int u) { return bag_base + r * step + u * per_round; };
+    auto idx_of = [&](int r, int u) {
+        int64_t b = bag_of(r, u);
+        b = b < batch ? b : batch - 1;  // keep every lane active
+        return d.idx[b * d.ld_idx];
+    };
+    int64_t iv[U];    // indices of round r + 1 (then r + 2)
+    u32x4 cur[U];     // rows of round r
+    bool okc[U];
+    int bad = 0;
+    // prologue: round 0's indices and rows, round 1's indices
+#pragma unroll
+    for (int u = 0; u < U; ++u) iv[u] = idx_of(0, u);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t row = (uint64_t)(iv[u] - 1);
+        okc[u] = row < (uint64_t)d.nrows;
+        cur[u] = reinterpret_cast<const u32x4*>(table + (okc[u] ? row * (uint64_t)ld_b : 0))[sub];
+    }
+    if (rounds > 1)
+#pragma unroll
+        for (int u = 0; u < U; ++u) iv[u] = idx_of(1, u);
+    for (int r = 0; r < rounds; ++r) {
+        if (bag_of(r, 0) >= batch) break;  // uniform per group: later rounds are past too
+        int64_t nx[U];
+        if (r + 2 < rounds)
+#pragma unroll
+            for (int u = 0; u < U; ++u) nx[u] = idx_of(r + 2, u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t bag = bag_of(r, u);
+            if (bag < batch) {
+                bad += okc[u] ? 0 : 1;
+                u32x4* o = reinterpret_cast<u32x4*>(dst + bag * ld_dst_b + d.dst_row_off * es) + sub;
+                store16<NT>(o, okc[u] ? cur[u] : u32x4{0u, 0u, 0u, 0u});
+            }
+        }
+        if (r + 1 < rounds) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t row = (uint64_t)(iv[u] - 1);
+                okc[u] = row < (uint64_t)d.nrows;
+                cur[u] = reinterpret_cast<const u32x4*>(table + (okc[u] ? row * (uint64_t)ld_b : 0))[sub];
+            }
+        }
+        if (r + 2 < rounds)
+#pragma unroll
+            for (int u = 0; u < U; ++u) iv[u] = nx[u];
+    }
+    if (bad && sub == 0) note_oob(bad);
+}
+
 // Generic path: any feature size / alignment / per-table dims / paged tables.  One wave
 // per bag, lanes stride over the features, pool order sequential per feature.
 // Store conversion T -> O; bfloat16 converts through float (exact for 16-bit types).
@@ -1144,6 +1225,8 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     return ET_OK;
 }
 
+constexpr int kGatherPipeRounds = 2;
+
 template <int RB, bool NT>
 int launch_gather_rb(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                      int es, hipStream_t s) {
@@ -1152,6 +1235,19 @@ int launch_gather_rb(const LookupPack& pack, int n, int64_t batch, void* dst, in
     constexpr int NV = VPR / LPR;
     constexpr int U = NV >= 8 ? 1 : 8 / NV;
     const int64_t per_round = 4 * (64 / LPR) * U;
+    if constexpr (NV == 1 && U == 8) {
+        // pipelined over kGatherPipeRounds rounds (k_gather_pipe) when the launch still has
+        // at least 256 workgroups; ET_GATHER_PIPE (experiment builds) sets the rounds, 1 = off
+        const int pr = (int)ET_KNOB("ET_GATHER_PIPE", kGatherPipeRounds);
+        const int64_t g = (batch + per_round * pr - 1) / (per_round * pr) * n;
+        if (pr > 1 && g >= 256) {
+            if (g > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+            hipLaunchKernelGGL((k_gather_pipe<RB, NT>), dim3((unsigned)g), dim3(256), 0, s, pack,
+                               n, batch, reinterpret_cast<char*>(dst), ld_dst * es, es, pr);
+            ET_LAUNCH_CHECK("k_gather_pipe");
+            return ET_OK;
+        }
+    }
     const int rounds = rounds_for(batch, per_round, n);
     const int64_t nchunks = (batch + per_round * rounds - 1) / (per_round * rounds);
     const int64_t grid = nchunks * n;

@@ -1192,29 +1192,29 @@ __device__ __forceinline__ uint32_t run_length(const uint32_t* __restrict__ bags
 }
 
 // A tile's place: its column m, the column's occurrence range, the tile's first
-// occurrence and its index among the column's tiles.
+// occurrence, its index among the column's tiles and their count, and the table — one
+// 32-byte record per tile, written by k_chain_tile_fill (so k_chain_tcount / k_chain_emit
+// read one record instead of following tile -> column -> segment -> key -> table, five
+// dependent loads per tile beside the chunk pass).
 struct ChainTile {
     uint32_t m, ss, se, a, ti, nt;
     int t;  // table
+    uint32_t pad;
 };
+static_assert(sizeof(ChainTile) == 32, "tile record");
 
-__device__ __forceinline__ ChainTile chain_tile(const UpdatePack& pack, int ntables,
-                                                const uint32_t* __restrict__ keys,
-                                                const uint32_t* __restrict__ seg_start,
-                                                const uint32_t* __restrict__ mlist,
-                                                const uint32_t* __restrict__ tile0,
-                                                const uint32_t* __restrict__ tile_col,
-                                                uint32_t M, uint32_t T, uint32_t tile) {
+__device__ __forceinline__ ChainTile chain_tile(const ChainTile* __restrict__ recs, uint32_t tile) {
+    const uint4* p = reinterpret_cast<const uint4*>(recs + tile);
+    const uint4 x = p[0], y = p[1];
     ChainTile c;
-    c.m = tile_col[tile];
-    const uint32_t u = mlist[c.m];
-    c.ss = seg_start[u];
-    c.se = seg_start[u + 1];
-    const uint32_t t0 = tile0[c.m];
-    c.ti = tile - t0;
-    c.nt = (c.m + 1 < M ? tile0[c.m + 1] : T) - t0;
-    c.a = c.ss + c.ti * kChainTile;
-    c.t = table_of_key(pack, ntables, keys[c.ss]);
+    c.m = x.x;
+    c.ss = x.y;
+    c.se = x.z;
+    c.a = x.w;
+    c.ti = y.x;
+    c.nt = y.y;
+    c.t = (int)y.z;
+    c.pad = 0u;
     return c;
 }
 
@@ -1301,16 +1301,27 @@ __global__ __launch_bounds__(256) void k_chain_tile_count(UpdatePack pack, int n
     }
 }
 
-// Index phase 1b (grid, after the exclusive scan of tile0): the tile -> column map and the
-// tile total (counters[kCntT] = tile0[M]).
-__global__ __launch_bounds__(256) void k_chain_tile_fill(const uint32_t* __restrict__ tile0,
+// Index phase 1b (grid, after the exclusive scan of tile0): the tile records (ChainTile)
+// and the tile total (counters[kCntT] = tile0[M]).
+__global__ __launch_bounds__(256) void k_chain_tile_fill(UpdatePack pack, int ntables,
+                                                         const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ seg_start,
+                                                         const uint32_t* __restrict__ mlist,
+                                                         const uint32_t* __restrict__ tile0,
                                                          uint32_t* __restrict__ counters,
-                                                         uint32_t* __restrict__ tile_col) {
+                                                         ChainTile* __restrict__ recs) {
     const uint32_t M = counters[kCntM];
     if (blockIdx.x == 0 && threadIdx.x == 0) counters[kCntT] = tile0[M];
     for (uint32_t m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
         const uint32_t t0 = tile0[m], t1 = tile0[m + 1];
-        for (uint32_t k = t0; k < t1; ++k) tile_col[k] = m;
+        if (t0 == t1) continue;
+        const uint32_t u = mlist[m], ss = seg_start[u], se = seg_start[u + 1];
+        const uint32_t t = (uint32_t)table_of_key(pack, ntables, keys[ss]);
+        for (uint32_t k = t0; k < t1; ++k) {
+            uint4* p = reinterpret_cast<uint4*>(recs + k);
+            p[0] = make_uint4(m, ss, se, ss + (k - t0) * kChainTile);
+            p[1] = make_uint4(k - t0, t1 - t0, t, 0u);
+        }
     }
 }
 
@@ -1322,15 +1333,14 @@ __global__ __launch_bounds__(256) void k_chain_tcount(UpdatePack pack, int ntabl
                                                       const uint32_t* __restrict__ mlist,
                                                       const uint32_t* __restrict__ counters,
                                                       const uint32_t* __restrict__ tile0,
-                                                      const uint32_t* __restrict__ tile_col,
+                                                      const ChainTile* __restrict__ trec,
                                                       uint32_t* __restrict__ tcnt) {
     __shared__ uint32_t bags[kChainLds];
     __shared__ uint32_t red[4][5];
     const uint32_t M = counters[kCntM], T = counters[kCntT];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
-        const ChainTile c = chain_tile(pack, ntables, keys, seg_start, mlist, tile0, tile_col, M,
-                                       T, tile);
+        const ChainTile c = chain_tile(trec, tile);
         const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
         const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
         stage_bags(bags, vals, c.ss, c.se, c.a, occ_off, pool);
@@ -1402,7 +1412,12 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
 // Index phase 4 (one workgroup): entry offsets (exclusive scan of the padded counts) and
 // the dispatch order: columns bucketed by log2 of their cost (entries x (S + overhead)),
 // costliest bucket first; the order inside a bucket is arbitrary (results never depend
-// on which wave takes a column).
+// on which wave takes a column).  The counts come kPlanU x 256 at a time (coalesced, all
+// loads issued before the first scan), so the loop waits for memory once per kPlanU block
+// scans (round 4 waited once per scan: 67-108 us beside the chunk pass; thread-contiguous
+// runs instead, uncoalesced: 205 us).
+constexpr int kPlanU = 8;
+
 __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __restrict__ counters,
                                                      const uint32_t* __restrict__ cnt,
                                                      const uint2* __restrict__ info,
@@ -1413,22 +1428,31 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __r
     const uint32_t M = counters[kCntM];
     if (threadIdx.x < 65) hist[threadIdx.x] = 0u;
     __syncthreads();
-    auto bucket = [&](uint32_t m) {  // leading zeros of the cost: 0 = costliest, 64 = none
-        const uint2 in = info[m];
+    auto bucket = [&](uint2 in) {  // leading zeros of the cost: 0 = costliest, 64 = none
         const uint64_t c = (uint64_t)in.y * chain_entry_cost2(in.x);
         return c ? (uint32_t)__clzll((long long)c) : 64u;
     };
     uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads) {
-        const uint32_t m = b0 + threadIdx.x;
-        const uint32_t v = m < M ? cnt[m] : 0u;
-        uint32_t total;
-        const uint32_t inc = block_inclusive_scan<kPlanThreads / 64>(v, lds16, &total);
-        if (m < M) {
-            e0[m] = carry + inc - v;
-            atomicAdd(&hist[bucket(m)], 1u);
+    for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads * kPlanU) {
+        uint32_t v[kPlanU];
+        uint2 in[kPlanU];
+#pragma unroll
+        for (int u = 0; u < kPlanU; ++u) {
+            const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
+            v[u] = m < M ? cnt[m] : 0u;
+            in[u] = m < M ? info[m] : make_uint2(0u, 0u);
         }
-        carry += total;
+#pragma unroll
+        for (int u = 0; u < kPlanU; ++u) {
+            const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
+            uint32_t total;
+            const uint32_t inc = block_inclusive_scan<kPlanThreads / 64>(v[u], lds16, &total);
+            if (m < M) {
+                e0[m] = carry + inc - v[u];
+                atomicAdd(&hist[bucket(in[u])], 1u);
+            }
+            carry += total;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1440,8 +1464,18 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __r
         }
     }
     __syncthreads();
-    for (uint32_t m = threadIdx.x; m < M; m += kPlanThreads) {
-        order[atomicAdd(&hist[bucket(m)], 1u)] = m;
+    for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads * kPlanU) {
+        uint2 in[kPlanU];
+#pragma unroll
+        for (int u = 0; u < kPlanU; ++u) {
+            const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
+            in[u] = m < M ? info[m] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kPlanU; ++u) {
+            const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
+            if (m < M) order[atomicAdd(&hist[bucket(in[u])], 1u)] = m;
+        }
     }
 }
 
@@ -1465,7 +1499,7 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
                                                     const uint32_t* __restrict__ mlist,
                                                     const uint32_t* __restrict__ counters,
                                                     const uint32_t* __restrict__ tile0,
-                                                    const uint32_t* __restrict__ tile_col,
+                                                    const ChainTile* __restrict__ trec,
                                                     const uint32_t* __restrict__ tcnt,
                                                     const uint32_t* __restrict__ cnt,
                                                     const uint2* __restrict__ info,
@@ -1478,8 +1512,7 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
     const uint32_t M = counters[kCntM], T = counters[kCntT];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
-        const ChainTile c = chain_tile(pack, ntables, keys, seg_start, mlist, tile0, tile_col, M,
-                                       T, tile);
+        const ChainTile c = chain_tile(trec, tile);
         const uint2 in = info[c.m];
         const uint32_t S = in.x, kS = (uint32_t)(__ffs((int)S) - 1);
         const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
@@ -1633,20 +1666,33 @@ __global__ __launch_bounds__(1024) void k_eh_pick(UpdatePack pack, EcList ec, ui
     __syncthreads();
     const int64_t nb = d.batch < kEhSampleBags ? d.batch : kEhSampleBags;
     const int64_t nocc = nb * d.pool;
-    for (int64_t o = threadIdx.x; o < nocc; o += 1024) {
-        const int64_t b = o / d.pool, j = o - b * d.pool;
-        const uint64_t c = (uint64_t)(d.idx[b * d.ld_idx + j] - 1);
-        if (c >= (uint64_t)d.nrows) continue;
-        uint32_t h = ((uint32_t)c * 2654435761u) >> 20;  // 12 bits
-        for (int probe = 0; probe < kEhProbes; ++probe, h = (h + 1) & (kEhHash - 1)) {
-            // the hot columns' slots are taken early: a plain read finds them without a CAS
-            const uint32_t seen = hk[h];
-            const uint32_t prev = seen == (uint32_t)c ? seen : atomicCAS(&hk[h], ~0u, (uint32_t)c);
-            if (prev == ~0u || prev == (uint32_t)c) {
-                atomicAdd(&hc[h], 1u);
-                break;
-            }
-        }  // a crowded neighbourhood drops the occurrence: the sample only ranks columns
+    // kEhPickU index loads in flight per thread before the hash updates (round 4 loaded one
+    // index per hash update: 20 dependent rounds of memory latency, 214 us beside the index phase)
+    constexpr int kEhPickU = 5;
+    for (int64_t o0 = threadIdx.x; o0 < nocc; o0 += 1024 * kEhPickU) {
+        uint64_t cs[kEhPickU];
+#pragma unroll
+        for (int u = 0; u < kEhPickU; ++u) {
+            const int64_t o = o0 + 1024 * u;
+            const int64_t b = o / d.pool, j = o - b * d.pool;
+            cs[u] = o < nocc ? (uint64_t)(d.idx[b * d.ld_idx + j] - 1) : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < kEhPickU; ++u) {
+            const uint64_t c = cs[u];
+            if (c >= (uint64_t)d.nrows) continue;
+            uint32_t h = ((uint32_t)c * 2654435761u) >> 20;  // 12 bits
+            for (int probe = 0; probe < kEhProbes; ++probe, h = (h + 1) & (kEhHash - 1)) {
+                // the hot columns' slots are taken early: a plain read finds them without a CAS
+                const uint32_t seen = hk[h];
+                const uint32_t prev =
+                    seen == (uint32_t)c ? seen : atomicCAS(&hk[h], ~0u, (uint32_t)c);
+                if (prev == ~0u || prev == (uint32_t)c) {
+                    atomicAdd(&hc[h], 1u);
+                    break;
+                }
+            }  // a crowded neighbourhood drops the occurrence: the sample only ranks columns
+        }
     }
     __syncthreads();
     // expected total >= min_occ  <=>  sample count * batch >= min_occ * nb
@@ -1678,23 +1724,46 @@ __global__ __launch_bounds__(1024) void k_eh_pick(UpdatePack pack, EcList ec, ui
     }
 }
 
-// Per-bag column counts in LDS: row `tid` (bag blk * kEcBags + tid) holds r(c, bag) for
-// the table's R <= kEcMaxRows columns, one byte each (out-of-range indices are not
-// counted; the main index phase reports them).
+// Per-bag column counts in LDS: row `b` (bag blk * kEcBags + b) holds r(c, bag) for the
+// table's R <= kEcMaxRows columns, one byte each (out-of-range indices are not counted; the
+// main index phase reports them).  The block's indices are read flat — occurrence o of the
+// block is bag o / pool, position o % pool: coalesced, kEcHistU loads in flight per thread —
+// and counted with packed LDS atomics (a byte never carries: r <= pool <= 255).  (Round 4
+// walked one bag per thread, its pool loads one after another: k_ec_count 162 us on the EC
+// list and 202 us on the EH list beside the index phase.)
+constexpr int kEcHistU = 8;
+
 __device__ __forceinline__ void ec_hist(const et_update_desc& d, uint32_t blk, uint8_t* hist,
                                         uint32_t RS, const uint32_t* cand = nullptr) {
     const uint32_t R = (uint32_t)d.nrows, pool = (uint32_t)d.pool;
-    uint32_t* row = reinterpret_cast<uint32_t*>(hist + threadIdx.x * RS);
-    for (uint32_t i = 0; i < RS / 4; ++i) row[i] = 0u;
-    const int64_t b = (int64_t)blk * kEcBags + threadIdx.x;
-    if (b < d.batch) {
-        const int64_t* ip = d.idx + b * d.ld_idx;
-        uint8_t* h = hist + threadIdx.x * RS;
-        for (uint32_t j = 0; j < pool; ++j) {
-            const uint64_t c = (uint64_t)(ip[j] - 1);
-            if (c >= R) continue;
-            const int slot = cand ? eh_slot(cand, (uint32_t)c) : (int)c;  // EH: candidates only
-            if (slot >= 0) h[slot] = (uint8_t)(h[slot] + 1u);
+    uint32_t* h32 = reinterpret_cast<uint32_t*>(hist);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kEcBags * RS / 4u; i += kEcBags) h32[i] = 0u;
+    __syncthreads();
+    const int64_t b0 = (int64_t)blk * kEcBags;
+    const int64_t left = d.batch - b0;
+    const uint32_t nb = (uint32_t)(left < kEcBags ? left : kEcBags);
+    const uint32_t nocc = nb * pool;
+    const int64_t* base = d.idx + b0 * d.ld_idx;
+    const int64_t ldi = d.ld_idx;
+    for (uint32_t o0 = threadIdx.x; o0 < nocc; o0 += kEcHistU * kEcBags) {
+        int64_t v[kEcHistU];
+#pragma unroll
+        for (int u = 0; u < kEcHistU; ++u) {
+            const uint32_t o = o0 + (uint32_t)u * kEcBags;
+            const uint32_t b = o / pool;
+            v[u] = o < nocc ? base[(int64_t)b * ldi + (o - b * pool)] : 0;  // 0: not counted
+        }
+#pragma unroll
+        for (int u = 0; u < kEcHistU; ++u) {
+            const uint32_t o = o0 + (uint32_t)u * kEcBags;
+            const uint64_t c = (uint64_t)(v[u] - 1);
+            if (c < R) {
+                const int slot = cand ? eh_slot(cand, (uint32_t)c) : (int)c;  // EH: candidates
+                if (slot >= 0) {
+                    const uint32_t at = (o / pool) * RS + (uint32_t)slot;
+                    atomicAdd(&h32[at >> 2], 1u << (8u * (at & 3u)));
+                }
+            }
         }
     }
     __syncthreads();
@@ -1743,7 +1812,7 @@ __device__ __forceinline__ EcParts ec_parts(uint32_t R) {
 __global__ __launch_bounds__(256) void k_ec_count(UpdatePack pack, EcList ec,
                                                   uint32_t* __restrict__ stats,
                                                   const uint32_t* __restrict__ cand) {
-    __shared__ __attribute__((aligned(16))) uint8_t hist[kEcBags * kEcMaxRows];
+    extern __shared__ __attribute__((aligned(16))) uint8_t hist[];  // kEcBags x ec_rs(ec)
     __shared__ uint32_t red[kEcBags][6];
     __shared__ uint32_t sc[kEhK];
     const int e = ec_find(ec, blockIdx.x);
@@ -1875,7 +1944,7 @@ __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
                                                  const uint2* __restrict__ info,
                                                  uint32_t* __restrict__ ent,
                                                  const uint32_t* __restrict__ cand) {
-    __shared__ __attribute__((aligned(16))) uint8_t hist[kEcBags * kEcMaxRows];
+    extern __shared__ __attribute__((aligned(16))) uint8_t hist[];  // kEcBags x ec_rs(ec)
     __shared__ uint32_t psum[kEcBags];
     __shared__ uint32_t sc[kEhK];
     const int e = ec_find(ec, blockIdx.x);
@@ -1912,13 +1981,10 @@ __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
 // 128 entries.  The 64-entry chunk is loaded permuted (lane 16r + k holds entry 4k + r),
 // so DPP row_newbcast:k hands row r entry 4k + r.  Same adds in the same order as the
 // 64-feature loop (bit-identical); rows 1-3 add garbage that is never stored.
-// The ring holds R quads (R / 16 chunks): 32 (128 entries in flight) in the regular list,
-// whose waves share SIMDs with the chunk pass at 5 waves per SIMD (~100 VGPRs each), 64 (256
-// entries, 64 ring VGPRs) on the exclusive SIMDs of k_sgd_chains_x, whose waves have the
-// register file to themselves: the hot columns' walks are latency-bound, so twice the loads
-// in flight is twice the entries per microsecond until issue binds (~11 cycles per entry).
-constexpr int kQuadRing = 32;   // quads (4 entries each) of gradient loads in flight (default)
-constexpr int kQuadRingX = 64;  // the same on exclusive SIMDs (k_sgd_chains_x)
+// The ring holds R quads (R / 16 chunks, R = kQuadRing = 32: 128 entries in flight).  A
+// 64-quad ring on the exclusive SIMDs measured slower (config 4, one box: 3.874-3.877 ms at
+// 32 against 3.88-3.91 at 64, profiles/r05/exact_grid/ab_r05o.txt).
+constexpr int kQuadRing = 32;   // quads (4 entries each) of gradient loads in flight
 constexpr int kQuadItems = 4;   // work items per (column, 64-feature slice): 16-feature quarters
 constexpr int kQuadMinGroups = 1024;  // quad walk for S = 1 chains of >= 64 K entries
 
@@ -2065,7 +2131,7 @@ __device__ __forceinline__ C chain_walk_wide(const uint32_t* ent, uint32_t ngr, 
 // (the quad walk, 16 features each); any other chain takes the whole slice in quarter 0
 // (the other quarters return at once).  T is the table and gradient type, C the
 // accumulator (sgd_apply_t).
-template <typename T, typename C, int MODE, bool NT, int QR>
+template <typename T, typename C, int MODE, bool NT>
 __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntables,
                                                const ChainCol* __restrict__ chains,
                                                const uint32_t* __restrict__ order,
@@ -2101,7 +2167,7 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
             const int f = f0 + (lane & 15);
             const uint32_t fc = (uint32_t)(f < d.dim ? f : d.dim - 1);
             const uint32_t ld = (uint32_t)d.ld_delta;
-            const float acc = chain_walk_quad<QR>(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
+            const float acc = chain_walk_quad<kQuadRing>(e, c.ngr, c.ngr * kChainGroup + kChainPad, delta,
                                               (uint32_t)d.batch * ld * 4u, 4u * fc, 4u * ld);
             if (lane < 16 && f < d.dim) {
                 float* w = col_ptr<float>(d.table, d.ld_table, d.cols_per_page,
@@ -2158,7 +2224,7 @@ __device__ uint4 g_ctl[kCtlCap][2];
 __device__ uint32_t g_ctl_n;
 #endif
 
-template <typename T, typename C, int MODE, bool NT, int QR = kQuadRing>
+template <typename T, typename C, int MODE, bool NT>
 __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
                                             uint32_t* __restrict__ counters,
                                             const ChainCol* __restrict__ chains,
@@ -2176,8 +2242,8 @@ __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
 #ifdef ET_EXPERIMENTS
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        sgd_chain_item<T, C, MODE, NT, QR>(pack, ntables, chains, order, ent, ns, eta_c, eta64,
-                                           it, quad_min);
+        sgd_chain_item<T, C, MODE, NT>(pack, ntables, chains, order, ent, ns, eta_c, eta64, it,
+                                       quad_min);
 #ifdef ET_EXPERIMENTS
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
         const ChainCol c = chains[order[(it / (uint32_t)kQuadItems) / (uint32_t)ns]];
@@ -2226,15 +2292,15 @@ __global__ __launch_bounds__(512) void k_sgd_chains_w(
 // the singles, the index phase — can be resident on its SIMDs while it runs; the chain waves
 // then issue at the SIMD's own rate instead of sharing it (the early chains and the early hot
 // columns by default, kChainExcl).
-template <typename T, typename C, int MODE, bool NT, int QR>
+template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chains_x(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
     const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
     uint32_t list) {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
-    chain_items<T, C, MODE, NT, QR>(pack, ntables, counters, chains, order, ent, ns, eta_c,
-                                    eta64, quad_min, list);
+    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
+                                quad_min, list);
 }
 
 // The rest of the update phase of an exact Float32 call in one launch: blocks [0, nch)
@@ -2351,7 +2417,8 @@ struct UpdateWs {
     uint2* chain_info;
     // the index phase's tiles: first tile per column, tile -> column, entries per tile at
     // S = 1..16
-    uint32_t *chain_tile0, *chain_tile_col, *chain_tcnt;
+    uint32_t *chain_tile0, *chain_tcnt;
+    ChainTile* chain_trec;
     uint32_t* chain_part;  // the regular plan's scan partials (its own: it runs beside others)
     // early chains (EcList): per (column, block) stats and entry offsets, per EC column the
     // padded entry count, (S, entries), descriptor and cost order, their entries, and a
@@ -2422,7 +2489,7 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
     const int64_t tmax = chain_tiles_max(n, chunk);
     w.chain_tile0 = (uint32_t*)take(4 * (mmax + 1));
     w.chain_part = (uint32_t*)take(4 * scan_part_entries(mmax + 1));
-    w.chain_tile_col = (uint32_t*)take(4 * tmax);
+    w.chain_trec = (ChainTile*)take((int64_t)sizeof(ChainTile) * tmax);
     w.chain_tcnt = (uint32_t*)take(20 * tmax);
     auto carve_ec = [&](const EcList* l, int64_t occ) {
         const int64_t recs = l && l->n ? l->cb0[l->n] : 0, M = l && l->n ? l->col0[l->n] : 0;
@@ -2508,11 +2575,11 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
     int rc = exclusive_scan_u32(w.chain_tile0, w.chain_tile0, mmax + 1, w.chain_part, s,
                                 w.counters + kCntM, 1);
     if (rc != ET_OK) return rc;
-    hipLaunchKernelGGL(k_chain_tile_fill, dim3(mg), dim3(256), 0, s, w.chain_tile0, w.counters,
-                       w.chain_tile_col);
+    hipLaunchKernelGGL(k_chain_tile_fill, dim3(mg), dim3(256), 0, s, pack, ntables, out.keys,
+                       w.seg_start, w.mlist, w.chain_tile0, w.counters, w.chain_trec);
     hipLaunchKernelGGL(k_chain_tcount, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                        out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                       w.chain_tile_col, w.chain_tcnt);
+                       w.chain_trec, w.chain_tcnt);
     hipLaunchKernelGGL(k_chain_choose, dim3(cg), dim3(256), 0, s, out.keys, w.seg_start,
                        w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
                        w.chain_info, w.chains, 4);
@@ -2520,7 +2587,7 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
                        w.chain_info, w.chain_e0, w.chain_order);
     hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                        out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
-                       w.chain_tile_col, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
+                       w.chain_trec, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
                        w.chain_ent, w.chains);
     ET_LAUNCH_CHECK("k_chain_emit");
     // ET_CHAIN_CHECK (experiment builds): validate every entry of the plan
@@ -2687,15 +2754,9 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
     ET_HIP_CHECK(attr);
     static const hipError_t attr_x = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT, kQuadRingX>),
+        reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
     ET_HIP_CHECK(attr_x);
-#ifdef ET_EXPERIMENTS
-    static const hipError_t attr_x32 = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&k_sgd_chains_x<T, C, MODE, NT, kQuadRing>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
-    ET_HIP_CHECK(attr_x32);
-#endif
     static const hipError_t attr_w = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&k_sgd_chains_w<T, C, MODE, NT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)kChainReserveLds);
@@ -2709,16 +2770,7 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
         return ET_OK;
     }
     if (excl) {
-#ifdef ET_EXPERIMENTS
-        if (ET_KNOB("ET_QUAD_RING_X", kQuadRingX) != kQuadRingX) {  // the 32-quad ring
-            hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT, kQuadRing>), dim3(nb), dim3(256),
-                               kChainReserveLds, s, pack, ntables, counters, chains, order, ent,
-                               ns, eta_c, eta64, quad_min, list);
-            ET_LAUNCH_CHECK("k_sgd_chains_x");
-            return ET_OK;
-        }
-#endif
-        hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT, kQuadRingX>), dim3(nb), dim3(256),
+        hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT>), dim3(nb), dim3(256),
                            kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
                            eta_c, eta64, quad_min, list);
         ET_LAUNCH_CHECK("k_sgd_chains_x");
@@ -3149,15 +3201,22 @@ inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chu
         if (cand_ready) ET_HIP_CHECK(hipEventRecord(cand_ready, s));
     }
     ET_HIP_CHECK(hipMemsetAsync(w.counters, 0, 4 * kCntSlots, s));
-    hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.stats,
-                       cand_c);
+    // the byte histogram in dynamic LDS, sized for the list's widest table (EH: kEhK slots)
+    uint32_t rs = 4;
+    for (int e = 0; e < ec.n; ++e) {
+        const uint32_t r = (ec.col0[e + 1] - ec.col0[e] + 3u) & ~3u;
+        rs = r > rs ? r : rs;
+    }
+    const size_t hist_lds = (size_t)kEcBags * rs;
+    hipLaunchKernelGGL(k_ec_count, dim3(ec.blk0[ec.n]), dim3(kEcBags), hist_lds, s, pack, ec,
+                       w.stats, cand_c);
     hipLaunchKernelGGL(k_ec_plan, dim3((M + 3u) / 4u), dim3(256), 0, s, pack, ec, chunk,
                        w.stats, w.boff, w.cnt, w.nocc, w.info, w.chains, w.ent, w.counters, 4,
                        cand_c);
     hipLaunchKernelGGL(k_ec_order, dim3(1), dim3(1024), 0, s, ec, w.info, ns, w.order,
                        w.counters);
-    hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), 0, s, pack, ec, w.boff,
-                       w.info, w.ent, cand_c);
+    hipLaunchKernelGGL(k_ec_emit, dim3(ec.blk0[ec.n]), dim3(kEcBags), hist_lds, s, pack, ec,
+                       w.boff, w.info, w.ent, cand_c);
     ET_LAUNCH_CHECK("k_ec_emit");
     return ET_OK;
 }
