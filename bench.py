@@ -239,6 +239,12 @@ def table_classes(et, tables, idx, tids, batch, stream, mixed_ms, steps=10, warm
                      "algorithmic_GBs": alg / (ms * 1e-3) / 1e9,
                      "hbm_compulsory_GBs": hbm / (ms * 1e-3) / 1e9,
                      "hbm_compulsory_frac": hbm / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        tr = load_class_traffic(name)
+        if tr and tr.get("hbm_bytes_per_launch"):  # committed per-class PMC (same launch alone)
+            fb = tr["hbm_bytes_per_launch"]
+            out[name].update({"fabric_bytes_per_launch": fb, "fabric_GBs": fb / (ms * 1e-3) / 1e9,
+                              "fabric_over_compulsory": fb / hbm,
+                              "l2_hit_rate": tr.get("l2_hit_rate"), "traffic_source": tr["file"]})
         total += ms
         del dst
     out["sum_alone_ms"] = total
@@ -524,6 +530,23 @@ def bench_config3_fp16(et, L, tids, idx, device, steps, warmup, batch):
     del tabs, dst
     torch.cuda.empty_cache()
     return out
+
+
+def load_class_traffic(name):
+    """The latest committed PMC traffic of one headline table class launched alone
+    (profiles/rNN/classpmc/traffic_<class>.json: tools/class_pmc.py + tools/traffic.py)."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "classpmc",
+                                              f"traffic_{name}.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+            doc["file"] = os.path.relpath(path, REPO)
+            return doc
+        except (OSError, ValueError):
+            continue
+    return None
 
 
 def load_traffic():

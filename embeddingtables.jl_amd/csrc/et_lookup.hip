@@ -834,7 +834,7 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
 // are loaded before round r's are stored, and round r + 2's indices before those, so each
 // wave keeps a round of rows in flight while it writes the previous one.  The one-round
 // kernel loads every row of the launch, then stores them all: reads and writes never overlap
-// (config 2: 18.5 us per launch for 67.6 MB, compulsory traffic only, PMC
+// (config 2: 18.5 us per kernel for 67.6 MB, compulsory traffic only by PMC; pipelined: 15.5,
 // profiles/r05/cfg2/).  Vector memory counters retire in issue order, so the issue order is
 // indices(r + 2), store(r), rows(r + 1): the store waits only for round r's rows, the row
 // addresses of round r + 1 only for indices issued before them.  Rows of 16 * LPR bytes, one
@@ -1225,6 +1225,8 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     return ET_OK;
 }
 
+// Config 2, graph-replayed (tools/cfg2_trace.py, one box, twice): 1 round (k_gather_vec)
+// 19.21 us per launch, 2 rounds 16.00-16.02, 4 rounds 17.00-17.04 (profiles/r05/cfg2/).
 constexpr int kGatherPipeRounds = 2;
 
 template <int RB, bool NT>

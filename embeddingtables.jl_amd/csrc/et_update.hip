@@ -1418,6 +1418,27 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
 // runs instead, uncoalesced: 205 us).
 constexpr int kPlanU = 8;
 
+// Wave-aggregated LDS counter: every active lane adds 1 to h[key]; returns the counter's value
+// before this lane's increment (lanes of one key get consecutive values).  One atomic per
+// distinct key of the wave instead of one per lane (a cost bucket is shared by most of a
+// wave's columns, so per-lane atomics on it serialise).
+__device__ __forceinline__ uint32_t wave_hist_add(uint32_t* h, uint32_t key) {
+    const int lane = threadIdx.x & 63;
+    uint32_t mine = 0;
+    uint64_t todo = __ballot(1);
+    while (todo) {
+        const int lead = __ffsll((long long)todo) - 1;
+        const uint32_t k = (uint32_t)__shfl((int)key, lead, 64);
+        const uint64_t same = __ballot(key == k) & todo;
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(&h[k], (uint32_t)__popcll(same));
+        base = (uint32_t)__shfl((int)base, lead, 64);
+        if (key == k) mine = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+        todo &= ~same;
+    }
+    return mine;
+}
+
 __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __restrict__ counters,
                                                      const uint32_t* __restrict__ cnt,
                                                      const uint2* __restrict__ info,
@@ -1449,7 +1470,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __r
             const uint32_t inc = block_inclusive_scan<kPlanThreads / 64>(v[u], lds16, &total);
             if (m < M) {
                 e0[m] = carry + inc - v[u];
-                atomicAdd(&hist[bucket(in[u])], 1u);
+                wave_hist_add(hist, bucket(in[u]));
             }
             carry += total;
         }
@@ -1474,7 +1495,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __r
 #pragma unroll
         for (int u = 0; u < kPlanU; ++u) {
             const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
-            if (m < M) order[atomicAdd(&hist[bucket(in[u])], 1u)] = m;
+            if (m < M) order[wave_hist_add(hist, bucket(in[u]))] = m;
         }
     }
 }

@@ -12,7 +12,7 @@
 #   exact            kernel trace of one exact config-4 update + its timeline
 #   cfg2             config 2: kernel trace (graph and eager: duration vs gap) + PMC traffic
 #   classpmc         PMC traffic + time of each headline table class alone (tools/class_pmc.py)
-#   lookab:LIB:S1;S2:N  the headline launch (kernel ms) with library LIB and env sets S1, S2
+#   lookab:LIB:S1/S2:N  the headline launch (kernel ms) with library LIB and env sets S1, S2
 #                    (VAR=V,VAR=V; NONE=0 for none), alternating N times
 #   expexact:VAR=V,..  the exact step with the experiment build and env VAR=V
 #   upd:N            the config-4 update alone, N processes (tools/upd_only.py)
@@ -86,7 +86,7 @@ print('$c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric', roun
         timeout -k 10 200 rocprofv3 --kernel-trace -d "$D/trace_$m" -o run --output-format csv \
           -- python3 tools/cfg2_trace.py 20 $arg > "$D/time_$m.json" 2> "$D/trace_$m.err" || die cfg2 "$D/trace_$m.err"
         f=$(ls "$D"/trace_$m/*/run_kernel_trace.csv "$D"/trace_$m/run_kernel_trace.csv 2>/dev/null | head -1)
-        python3 tools/kgaps.py "$f" k_gather_vec 64 > "$D/gaps_$m.json"
+        python3 tools/kgaps.py "$f" k_gather 64 > "$D/gaps_$m.json"
         echo "$m $(cat "$D/time_$m.json") $(cat "$D/gaps_$m.json")"
       done
       for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
@@ -94,12 +94,12 @@ print('$c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric', roun
         timeout -s KILL 100 rocprofv3 --pmc $grp -d "$D/$tag" -o run --output-format csv \
           -- python3 tools/cfg2_trace.py 5 --eager > "$D/$tag.log" 2>&1 || die "cfg2 $tag" "$D/$tag.log"
       done
-      python3 tools/traffic.py "$D" k_gather_vec cfg2 "$D/traffic.json" | cut -c1-400 ;;
+      python3 tools/traffic.py "$D" k_gather cfg2 "$D/traffic.json" | cut -c1-400 ;;
     cfg2ab:*)
       # config 2 (graph-replayed, tools/cfg2_trace.py) with the experiment build and env sets
       IFS=: read -r _ SETSALL N <<< "$step"
       for i in $(seq 1 "${N:-2}"); do
-        for SETS in $(echo "$SETSALL" | tr ';' ' '); do
+        for SETS in $(echo "$SETSALL" | tr "/" " "); do
           env ET_LIBRARY=$EXP $(echo "$SETS" | tr ',' ' ') timeout -k 10 200 python3 tools/cfg2_trace.py 40 \
             > "$OUT/cfg2ab.json" 2> "$OUT/cfg2ab.err" || die cfg2ab "$OUT/cfg2ab.err"
           echo "$SETS $(cat "$OUT/cfg2ab.json")"
@@ -109,7 +109,7 @@ print('$c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric', roun
       # the headline launch with experiment library A and env sets (VAR=V,...;VAR=V,...), N rounds
       IFS=: read -r _ LIBV SETSALL N <<< "$step"
       for i in $(seq 1 "${N:-2}"); do
-        for SETS in $(echo "$SETSALL" | tr ';' ' '); do
+        for SETS in $(echo "$SETSALL" | tr "/" " "); do
           env ET_LIBRARY=$LIBV $(echo "$SETS" | tr ',' ' ') timeout -k 10 200 python3 bench.py --steps 40 --warmup 5 \
             --cpu-seconds 0 --no-extra --no-check > "$OUT/lookab.json" 2> "$OUT/lookab.err" || die lookab "$OUT/lookab.err"
           python3 -c "import json; d=json.load(open('$OUT/lookab.json')); print('$SETS', round(d['roofline']['kernel_ms'],4), round(d['roofline']['kernel_ms_median'],4))"
