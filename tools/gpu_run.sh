@@ -42,6 +42,12 @@ for step in "$@"; do
       timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
         -k "${step#tests:}" > "$OUT/pytest_k.log" 2>&1 || die tests "$OUT/pytest_k.log"
       tail -1 "$OUT/pytest_k.log" ;;
+    exptests:*)
+      # pytest -m gpu -k EXPR with the experiment build and env VAR=V,..: exptests:VAR=V,..:EXPR
+      IFS=: read -r _ SETS EXPR <<< "$step"
+      env ET_LIBRARY=$EXP $(echo "$SETS" | tr ',' ' ') timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v \
+        --timeout 300 --timeout-method thread -k "$EXPR" > "$OUT/pytest_exp.log" 2>&1 || die exptests "$OUT/pytest_exp.log"
+      echo "$SETS $(tail -1 "$OUT/pytest_exp.log")" ;;
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
         || die smoke "$OUT/smoke.log"
