@@ -8,6 +8,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            python bench.py (the driver's default run) -> bench.json
 #   trace            rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 3
+#   tracehead        the same with --no-extra (only the headline launches)
 #   pmc              PMC traffic of the headline kernel (tools/pmc_traffic.sh, tools/traffic.py)
 #   exact            kernel trace of one exact config-4 update + its timeline
 #   cfg2             config 2: kernel trace (graph and eager: duration vs gap) + PMC traffic
@@ -57,12 +58,18 @@ for step in "$@"; do
       python3 -c "import json,sys; d=json.load(open('$OUT/bench.json')); c=d.get('config4_zipf_update',{}); \
 print('bench', round(d['ms_per_step'],4), 'ms frac', round(d['roofline']['frac'],4), 'upd', round(c.get('update_exact_ms',0),3), \
 'split', round(c.get('update_split_ms',0),3), 'fp16', round(d.get('config3_fp16',{}).get('julia_f16_arith',{}).get('kernel_ms',0),4), \
-'cfg2', d.get('config2_gather',{}).get('us_per_launch'))" ;;
+'cfg2_us', round(1e3*d.get('config2_gather',{}).get('kernel_ms',0),2))" ;;
     trace)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run --output-format csv \
         -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 > "$OUT/bench_traced.json" \
         2> "$OUT/bench_traced.err" || die trace "$OUT/bench_traced.err"
       echo "trace ok" ;;
+    tracehead)
+      # the headline launch alone (no extra configs), so the kernel's rocprof average is its time
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_head" -o run --output-format csv \
+        -- python3 bench.py --steps 20 --warmup 3 --cpu-seconds 0 --no-extra > "$OUT/bench_head.json" \
+        2> "$OUT/bench_head.err" || die tracehead "$OUT/bench_head.err"
+      echo "tracehead ok" ;;
     pmc)
       bash tools/pmc_traffic.sh "$OUT/pmc" --steps 5 --warmup 1 --cpu-seconds 0 --no-extra || die pmc /dev/null
       python3 tools/traffic.py "$OUT/pmc" k_pooled_vec criteo26_b65536 "$OUT/pmc/traffic.json" | tail -1 ;;
