@@ -839,7 +839,7 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
 // indices(r + 2), store(r), rows(r + 1): the store waits only for round r's rows, the row
 // addresses of round r + 1 only for indices issued before them.  Rows of 16 * LPR bytes, one
 // vector per lane (NV = 1).  Bit copies, so any schedule gives the same bytes.
-template <int RB, bool NT>
+template <int RB, bool NT, bool NTL = false>
 __global__ __launch_bounds__(256) void k_gather_pipe(LookupPack pack, int ntables, int64_t batch,
                                                      char* __restrict__ dst, int64_t ld_dst_b,
                                                      int es, int rounds) {
@@ -876,7 +876,9 @@ __global__ __launch_bounds__(256) void k_gather_pipe(LookupPack pack, int ntable
     for (int u = 0; u < U; ++u) {
         const uint64_t row = (uint64_t)(iv[u] - 1);
         okc[u] = row < (uint64_t)d.nrows;
-        cur[u] = reinterpret_cast<const u32x4*>(table + (okc[u] ? row * (uint64_t)ld_b : 0))[sub];
+        const u32x4* src = reinterpret_cast<const u32x4*>(table + (okc[u] ? row * (uint64_t)ld_b : 0)) + sub;
+        if constexpr (NTL) cur[u] = __builtin_nontemporal_load(src);
+        else cur[u] = *src;
     }
     if (rounds > 1)
 #pragma unroll
@@ -901,7 +903,10 @@ __global__ __launch_bounds__(256) void k_gather_pipe(LookupPack pack, int ntable
             for (int u = 0; u < U; ++u) {
                 const uint64_t row = (uint64_t)(iv[u] - 1);
                 okc[u] = row < (uint64_t)d.nrows;
-                cur[u] = reinterpret_cast<const u32x4*>(table + (okc[u] ? row * (uint64_t)ld_b : 0))[sub];
+                const u32x4* src =
+                    reinterpret_cast<const u32x4*>(table + (okc[u] ? row * (uint64_t)ld_b : 0)) + sub;
+                if constexpr (NTL) cur[u] = __builtin_nontemporal_load(src);
+                else cur[u] = *src;
             }
         }
         if (r + 2 < rounds)
@@ -1244,6 +1249,19 @@ int launch_gather_rb(const LookupPack& pack, int n, int64_t batch, void* dst, in
         const int64_t g = (batch + per_round * pr - 1) / (per_round * pr) * n;
         if (pr > 1 && g >= 256) {
             if (g > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+            // rows of tables larger than the Infinity Cache load non-temporally, as the pooled
+            // kernels' (ntload_bytes): config 2 15.26-15.29 vs 15.99-16.04 us per launch
+            // (profiles/r05/cfg2/ab_gather_pipe.txt)
+            bool ntl = tuning().ntload != 0;
+            for (int t = 0; t < n && ntl; ++t)
+                ntl = pack.d[t].nrows * pack.d[t].ld_table * es > tuning().ntload_bytes;
+            if (ntl) {
+                hipLaunchKernelGGL((k_gather_pipe<RB, NT, true>), dim3((unsigned)g), dim3(256), 0,
+                                   s, pack, n, batch, reinterpret_cast<char*>(dst), ld_dst * es,
+                                   es, pr);
+                ET_LAUNCH_CHECK("k_gather_pipe");
+                return ET_OK;
+            }
             hipLaunchKernelGGL((k_gather_pipe<RB, NT>), dim3((unsigned)g), dim3(256), 0, s, pack,
                                n, batch, reinterpret_cast<char*>(dst), ld_dst * es, es, pr);
             ET_LAUNCH_CHECK("k_gather_pipe");
