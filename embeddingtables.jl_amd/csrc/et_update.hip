@@ -1676,6 +1676,7 @@ inline bool eh_enabled() { return ET_KNOB("ET_EH", 1) != 0; }
 // columns expected to reach kEhMinOcc occurrences, at most kEhK of them (the most frequent;
 // ties to the smaller column), and write them in ascending order, ~0 past the last.
 __global__ __launch_bounds__(1024) void k_eh_pick(UpdatePack pack, EcList ec, uint32_t min_occ,
+                                                  int64_t sample_bags,
                                                   uint32_t* __restrict__ cand) {
     __shared__ uint32_t hk[kEhHash], hc[kEhHash];
     __shared__ uint32_t qk[512], qc[512], nq;
@@ -1685,7 +1686,7 @@ __global__ __launch_bounds__(1024) void k_eh_pick(UpdatePack pack, EcList ec, ui
     for (int i = threadIdx.x; i < kEhHash; i += 1024) hk[i] = ~0u, hc[i] = 0u;
     if (threadIdx.x == 0) nq = 0u, nsel = 0u;
     __syncthreads();
-    const int64_t nb = d.batch < kEhSampleBags ? d.batch : kEhSampleBags;
+    const int64_t nb = d.batch < sample_bags ? d.batch : sample_bags;
     const int64_t nocc = nb * d.pool;
     // kEhPickU index loads in flight per thread before the hash updates (round 4 loaded one
     // index per hash update: 20 dependent rounds of memory latency, 214 us beside the index phase)
@@ -3217,7 +3218,10 @@ inline int launch_ec_plan(const UpdatePack& pack, const EcList& ec, uint32_t chu
     if (ec.hot) {
         // ET_EH_MIN (experiment builds): the expected occurrences of a candidate
         const uint32_t min_occ = (uint32_t)ET_KNOB("ET_EH_MIN", (long long)kEhMinOcc);
-        hipLaunchKernelGGL(k_eh_pick, dim3(ec.n), dim3(1024), 0, s, pack, ec, min_occ, cand);
+        // ET_EH_SAMPLE (experiment builds): bags sampled per table
+        const int64_t sample = ET_KNOB("ET_EH_SAMPLE", (long long)kEhSampleBags);
+        hipLaunchKernelGGL(k_eh_pick, dim3(ec.n), dim3(1024), 0, s, pack, ec, min_occ, sample,
+                           cand);
         ET_LAUNCH_CHECK("k_eh_pick");
         if (cand_ready) ET_HIP_CHECK(hipEventRecord(cand_ready, s));
     }
