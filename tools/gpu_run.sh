@@ -78,6 +78,14 @@ print('bench', round(d['ms_per_step'],4), 'ms frac', round(d['roofline']['frac']
         -- python3 tools/exact_cfg4.py exact > "$OUT/exact_traced.txt" 2>&1 || die exact "$OUT/exact_traced.txt"
       f=$(ls "$OUT"/prof_exact/*/run_kernel_trace.csv "$OUT"/prof_exact/run_kernel_trace.csv 2>/dev/null | head -1)
       python3 tools/upd_timeline.py "$f" > "$OUT/exact_timeline.txt" && grep -E "chains|sgd_exact|total" "$OUT/exact_timeline.txt" ;;
+    updpmc)
+      # fabric traffic per kernel of the exact config-4 update (tools/exact_cfg4.py, one call)
+      D=$OUT/updpmc; mkdir -p "$D"
+      for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+        timeout -s KILL 120 rocprofv3 --pmc $grp -d "$D/$grp" -o run --output-format csv \
+          -- python3 tools/exact_cfg4.py exact > "$D/$grp.log" 2>&1 || die "updpmc $grp" "$D/$grp.log"
+      done
+      python3 tools/kernel_traffic.py "$D" > "$D/per_kernel.txt" && head -25 "$D/per_kernel.txt" ;;
     classpmc)
       for c in heavy mid light all; do
         D=$OUT/classpmc/$c; mkdir -p "$D"
