@@ -1113,8 +1113,8 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
 // Index phase, over tiles of kChainTile occurrences so a 834,828-occurrence column is
 // cut by ~200 workgroups rather than walked by one wave: k_chain_tile_count/_fill (tiles per
 // column), k_chain_tcount (per tile, the entries its runs make at each S), k_chain_choose
-// (per column, S and the entry count), k_chain_plan (entry offsets, columns ordered by
-// cost so the longest chains are dispatched first), k_chain_emit (the entries).  Update phase: the chain role of
+// (per column, S and the entry count), k_chain_plan (entry offsets; columns in key order, the
+// early lists costliest first), k_chain_emit (the entries).  Update phase: the chain role of
 // k_sgd_exact, beside the chunk pass (single-chunk columns) and the singles in ONE
 // launch, so the hottest chains (834,828 adds on the config-4 batch) overlap the rest.
 
@@ -1409,59 +1409,28 @@ __global__ __launch_bounds__(256) void k_chain_choose(const uint32_t* __restrict
     }
 }
 
-// Index phase 4 (one workgroup): entry offsets (exclusive scan of the padded counts) and
-// the dispatch order: columns bucketed by log2 of their cost (entries x (S + overhead)),
-// costliest bucket first; the order inside a bucket is arbitrary (results never depend
-// on which wave takes a column).  The counts come kPlanU x 256 at a time (coalesced, all
-// loads issued before the first scan), so the loop waits for memory once per kPlanU block
-// scans (round 4 waited once per scan: 67-108 us beside the chunk pass; thread-contiguous
-// runs instead, uncoalesced: 205 us).
+// Index phase 4 (one workgroup): entry offsets (exclusive scan of the padded counts) and the
+// dispatch order — key order (table-major, ascending column), so the chains running at any
+// moment read the gradient rows of few tables and those stay in the Infinity Cache: config 4
+// 3.76-3.81 ms against 3.85-3.87 for round 4's costliest-first order (one box, A/B,
+// profiles/r05/exact_grid/ab_r05o.txt; the early lists keep costliest-first — in key order
+// their hottest chains start late: 4.01 / 4.70 ms).  The counts come kPlanU x 256 at a time
+// (coalesced, all loads issued before the first scan).
 constexpr int kPlanU = 8;
-
-// Wave-aggregated LDS counter: every active lane adds 1 to h[key]; returns the counter's value
-// before this lane's increment (lanes of one key get consecutive values).  One atomic per
-// distinct key of the wave instead of one per lane (a cost bucket is shared by most of a
-// wave's columns, so per-lane atomics on it serialise).
-__device__ __forceinline__ uint32_t wave_hist_add(uint32_t* h, uint32_t key) {
-    const int lane = threadIdx.x & 63;
-    uint32_t mine = 0;
-    uint64_t todo = __ballot(1);
-    while (todo) {
-        const int lead = __ffsll((long long)todo) - 1;
-        const uint32_t k = (uint32_t)__shfl((int)key, lead, 64);
-        const uint64_t same = __ballot(key == k) & todo;
-        uint32_t base = 0;
-        if (lane == lead) base = atomicAdd(&h[k], (uint32_t)__popcll(same));
-        base = (uint32_t)__shfl((int)base, lead, 64);
-        if (key == k) mine = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-        todo &= ~same;
-    }
-    return mine;
-}
 
 __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __restrict__ counters,
                                                      const uint32_t* __restrict__ cnt,
-                                                     const uint2* __restrict__ info,
                                                      uint32_t* __restrict__ e0,
                                                      uint32_t* __restrict__ order) {
     __shared__ uint32_t lds16[16];
-    __shared__ uint32_t hist[65];
     const uint32_t M = counters[kCntM];
-    if (threadIdx.x < 65) hist[threadIdx.x] = 0u;
-    __syncthreads();
-    auto bucket = [&](uint2 in) {  // leading zeros of the cost: 0 = costliest, 64 = none
-        const uint64_t c = (uint64_t)in.y * chain_entry_cost2(in.x);
-        return c ? (uint32_t)__clzll((long long)c) : 64u;
-    };
     uint32_t carry = 0;
     for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads * kPlanU) {
         uint32_t v[kPlanU];
-        uint2 in[kPlanU];
 #pragma unroll
         for (int u = 0; u < kPlanU; ++u) {
             const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
             v[u] = m < M ? cnt[m] : 0u;
-            in[u] = m < M ? info[m] : make_uint2(0u, 0u);
         }
 #pragma unroll
         for (int u = 0; u < kPlanU; ++u) {
@@ -1470,32 +1439,9 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __r
             const uint32_t inc = block_inclusive_scan<kPlanThreads / 64>(v[u], lds16, &total);
             if (m < M) {
                 e0[m] = carry + inc - v[u];
-                wave_hist_add(hist, bucket(in[u]));
+                order[m] = m;
             }
             carry += total;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int k = 0; k < 65; ++k) {
-            const uint32_t h = hist[k];
-            hist[k] = run;
-            run += h;
-        }
-    }
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < M; b0 += kPlanThreads * kPlanU) {
-        uint2 in[kPlanU];
-#pragma unroll
-        for (int u = 0; u < kPlanU; ++u) {
-            const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
-            in[u] = m < M ? info[m] : make_uint2(0u, 0u);
-        }
-#pragma unroll
-        for (int u = 0; u < kPlanU; ++u) {
-            const uint32_t m = b0 + (uint32_t)u * kPlanThreads + threadIdx.x;
-            if (m < M) order[wave_hist_add(hist, bucket(in[u]))] = m;
         }
     }
 }
@@ -1928,8 +1874,9 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
     for (uint32_t i = e0 + E + (uint32_t)lane; i < e0 + P; i += 64) ent[i] = pad;
 }
 
-// EC step 3 (one workgroup): the cost order of the EC columns (as k_chain_plan) and their
-// count (counters[kCntM], read by the chain role).
+// EC step 3 (one workgroup): the cost order of the EC columns — costliest first, so the
+// hottest chains start with the list — and their count (counters[kCntM], read by the chain
+// role).
 __global__ __launch_bounds__(1024) void k_ec_order(EcList ec, const uint2* __restrict__ info,
                                                    int ns,
                                                    uint32_t* __restrict__ order,
@@ -2606,7 +2553,7 @@ inline int launch_chain_plan(const UpdatePack& pack, int ntables, int64_t n, uin
                        w.mlist, w.counters, w.chain_tile0, w.chain_tcnt, w.chain_cnt,
                        w.chain_info, w.chains, 4);
     hipLaunchKernelGGL(k_chain_plan, dim3(1), dim3(kPlanThreads), 0, s, w.counters, w.chain_cnt,
-                       w.chain_info, w.chain_e0, w.chain_order);
+                       w.chain_e0, w.chain_order);
     hipLaunchKernelGGL(k_chain_emit, dim3(tg), dim3(256), 0, s, pack, ntables, out.keys,
                        out.vals, w.seg_start, w.mlist, w.counters, w.chain_tile0,
                        w.chain_trec, w.chain_tcnt, w.chain_cnt, w.chain_info, w.chain_e0,
