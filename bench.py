@@ -818,6 +818,8 @@ def main():
             if best is not runs[0]:
                 best["gpu_output_bit_identical"] = runs[0]["gpu_output_bit_identical"]
             result["cpu_baseline"] = best
+    if _lib.EXPERIMENT_BUILD:  # tools/ A/B runs only (ET_TOOLS_EXPERIMENT=1): say so
+        result["library"] = f"EXPERIMENT BUILD {_lib.LIB_PATH} (not the shipped library)"
     if rank == 0:
         print(json.dumps(result), flush=True)
     if sharded:

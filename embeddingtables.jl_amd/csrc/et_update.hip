@@ -1128,10 +1128,18 @@ __host__ __device__ constexpr uint32_t chain_entry_cost2(uint32_t S) {
     return S <= 1u ? 9u : S <= 4u ? 2u * S + 13u : 2u * S + 11u;
 }
 
-// A chain entry: r adds (r <= 16) of gradient column `bag` (< 2^24); padding is r = 0 at
-// bag = batch (past the gradient: the chain loop's range-checked load returns +0).
-__device__ __forceinline__ uint32_t chain_entry(uint32_t r, uint32_t bag) {
-    return r << 24 | bag;
+// A chain entry: r adds (r <= 16) of gradient column `bag`; padding is r = 0 at bag = batch
+// (past the gradient: the chain loop's range-checked load returns +0).  The bag takes the low
+// 24 bits (`r << 24 | bag`, the layout the Float32 asm and quad loops decode) when the table's
+// batch is below 2^24, else the low 27 (`r << 27 | bag`, r <= 16 still fits the top 5 bits;
+// read only by chain_walk_wide), so chains cover batches up to 2^27 - 1 bags.
+constexpr int64_t kChainNarrowBatch = 1ll << 24;
+constexpr int64_t kChainMaxBatch = (1ll << 27) - 1;
+__host__ __device__ __forceinline__ uint32_t chain_shift(int64_t batch) {
+    return batch < kChainNarrowBatch ? 24u : 27u;
+}
+__device__ __forceinline__ uint32_t chain_entry(uint32_t r, uint32_t bag, uint32_t sh) {
+    return r << sh | bag;
 }
 
 struct ChainCol {
@@ -1342,6 +1350,7 @@ __global__ __launch_bounds__(256) void k_chain_tcount(UpdatePack pack, int ntabl
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
         const ChainTile c = chain_tile(trec, tile);
         const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
+        const uint32_t sh = chain_shift(pack.d[c.t].batch);
         const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
         stage_bags(bags, vals, c.ss, c.se, c.a, occ_off, pool);
         __syncthreads();
@@ -1449,9 +1458,10 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __r
 // One run of r adds of delta column `bag` as ceil(r/S) entries (S adds each, the last
 // one the remainder).
 __device__ __forceinline__ void chain_put(uint32_t* __restrict__ ent, uint32_t at, uint32_t i,
-                                          uint32_t k, uint32_t r, uint32_t S, uint32_t bag) {
+                                          uint32_t k, uint32_t r, uint32_t S, uint32_t bag,
+                                          uint32_t sh) {
     const uint32_t adds = i + 1 < k ? S : r - S * (k - 1);
-    ent[at] = chain_entry(adds, bag);
+    ent[at] = chain_entry(adds, bag, sh);
 }
 
 // Index phase 5, per tile: the entries of the runs that start in it (after the entries
@@ -1483,6 +1493,7 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
         const uint2 in = info[c.m];
         const uint32_t S = in.x, kS = (uint32_t)(__ffs((int)S) - 1);
         const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
+        const uint32_t sh = chain_shift(pack.d[c.t].batch);
         const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
         stage_bags(bags, vals, c.ss, c.se, c.a, occ_off, pool);
         __syncthreads();
@@ -1508,12 +1519,12 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
             const uint32_t r = rl[j0 + j];
             if (r == 0u) continue;
             const uint32_t k = cdiv_u32(r, S), bag = bags[j0 + j + 1];
-            for (uint32_t i = 0; i < k; ++i) chain_put(ent, at + i, i, k, r, S, bag);
+            for (uint32_t i = 0; i < k; ++i) chain_put(ent, at + i, i, k, r, S, bag, sh);
             at += k;
         }
         if (c.ti + 1 == c.nt) {
             const uint32_t e0 = e0s[c.m], P = cnt[c.m];
-            const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[c.t].batch);
+            const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[c.t].batch, sh);
             for (uint32_t i = e0 + in.y + threadIdx.x; i < e0 + P; i += 256) ent[i] = pad;
             if (threadIdx.x == 0)
                 chains[c.m] = ChainCol{keys[c.ss], e0, (P - kChainPad) / kChainGroup, S};
@@ -1543,16 +1554,17 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
         if (c.S == 0u) continue;
         const int t = table_of_key(pack, ntables, c.key);
         const uint64_t lim = (uint64_t)pack.d[t].batch;
+        const uint32_t sh = chain_shift(pack.d[t].batch), bm = (1u << sh) - 1u;
         uint32_t bad = 0, real = 0, pad_then_real = 0;
         if (P != c.ngr * kChainGroup + kChainPad || c.S != info[m].x) bad = 1;
         for (uint32_t i = lane; i < P; i += 64) {
-            const uint32_t e = ent[c.e0 + i], r = e >> 24;
-            const bool ok = ((uint64_t)(e & 0xffffffu) < lim || (r == 0u && (e & 0xffffffu) == lim)) &&
+            const uint32_t e = ent[c.e0 + i], r = e >> sh;
+            const bool ok = ((uint64_t)(e & bm) < lim || (r == 0u && (e & bm) == lim)) &&
                             r <= c.S;
             // a bad entry becomes a padding entry (bag = batch: its range-checked load
             // returns +0), so the debug pass reports the violation without adding
             // gradient column 0 in its place (maskless S = 1 and quad walks add every entry)
-            if (!ok) ent[c.e0 + i] = chain_entry(0u, (uint32_t)lim);
+            if (!ok) ent[c.e0 + i] = chain_entry(0u, (uint32_t)lim, sh);
             bad += ok ? 0u : 1u;
             real += (ok && r > 0u) ? 1u : 0u;
             pad_then_real += (ok && r > 0u && i >= info[m].y) ? 1u : 0u;
@@ -1870,7 +1882,7 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
         if (b < nblk) boff[ec.cb0[e] + c * nblk + b] = carry + ex;
         carry += wave_sum_u32(x);
     }
-    const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[t].batch);
+    const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[t].batch, 24u);  // ec_table: batch <= 2^20
     for (uint32_t i = e0 + E + (uint32_t)lane; i < e0 + P; i += 64) ent[i] = pad;
 }
 
@@ -1935,7 +1947,7 @@ __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
         const uint32_t r = hist[i * q.RS + q.c];
         const uint32_t k = cdiv_u32(r, S);
         const uint32_t bag = blk * kEcBags + i;
-        for (uint32_t j = 0; j < k; ++j) chain_put(ent, at + j, j, k, r, S, bag);
+        for (uint32_t j = 0; j < k; ++j) chain_put(ent, at + j, j, k, r, S, bag, 24u);
         at += k;
     }
 }
@@ -2050,7 +2062,8 @@ __device__ __forceinline__ float chain_walk_quad(const uint32_t* ent, uint32_t n
 // (bag = batch) must land past the range to load +0 — so (batch + 1) * ld * 4 stays below
 // 2^32 and ld below 2^22.  Any other chain takes chain_walk_wide (64-bit addresses).
 __host__ __device__ inline bool chain_asm_ok(int64_t batch, int64_t ld) {
-    return ld < (1ll << 22) && (uint64_t)(batch + 1) * (uint64_t)ld * 4u < (1ull << 32);
+    return batch < kChainNarrowBatch && ld < (1ll << 22) &&
+           (uint64_t)(batch + 1) * (uint64_t)ld * 4u < (1ull << 32);
 }
 
 // The serial sum of one chain over one 64-feature slice (lane = feature), with 64-bit
@@ -2064,30 +2077,32 @@ __host__ __device__ inline bool chain_asm_ok(int64_t batch, int64_t ld) {
 constexpr int kWideAhead = 16;
 
 template <typename T>
-__device__ __forceinline__ T wide_load(const T* delta, uint64_t ld, uint32_t fc, uint32_t e) {
-    const uint64_t bag = (e >> 24) ? (uint64_t)(e & 0xffffffu) : 0u;
+__device__ __forceinline__ T wide_load(const T* delta, uint64_t ld, uint32_t fc, uint32_t e,
+                                       uint32_t sh) {
+    const uint64_t bag = (e >> sh) ? (uint64_t)(e & ((1u << sh) - 1u)) : 0u;
     return delta[bag * ld + fc];
 }
 
+// sh: the entries' bag width (chain_shift of the table's batch).
 template <typename T, typename C>
 __device__ __forceinline__ C chain_walk_wide(const uint32_t* ent, uint32_t ngr, const T* delta,
-                                             uint64_t ld, uint32_t fc, C acc) {
+                                             uint64_t ld, uint32_t fc, C acc, uint32_t sh) {
     static_assert(kChainGroup % kWideAhead == 0 && kChainPad >= kWideAhead, "wide walk layout");
     uint32_t en[kWideAhead];
     T x[kWideAhead];
 #pragma unroll
     for (int k = 0; k < kWideAhead; ++k) {
         en[k] = ent[k];
-        x[k] = wide_load(delta, ld, fc, en[k]);
+        x[k] = wide_load(delta, ld, fc, en[k], sh);
     }
     const uint32_t ne = ngr * (uint32_t)kChainGroup;
     for (uint32_t h = 0; h < ne; h += kWideAhead) {
 #pragma unroll
         for (int k = 0; k < kWideAhead; ++k) {
-            const uint32_t r = en[k] >> 24;
+            const uint32_t r = en[k] >> sh;
             const C v = C(x[k]);
             en[k] = ent[h + kWideAhead + k];  // inside the padding past the last trip
-            x[k] = wide_load(delta, ld, fc, en[k]);
+            x[k] = wide_load(delta, ld, fc, en[k], sh);
             for (uint32_t j = 0; j < r; ++j) acc = acc + v;
         }
     }
@@ -2166,7 +2181,9 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
             done = true;
         }
     }
-    if (!done) acc = chain_walk_wide<T, C>(e, c.ngr, delta, (uint64_t)d.ld_delta, fc, acc);
+    if (!done)
+        acc = chain_walk_wide<T, C>(e, c.ngr, delta, (uint64_t)d.ld_delta, fc, acc,
+                                    chain_shift(d.batch));
     if (f < d.dim) {
         T* w = col_ptr<T>(d.table, d.ld_table, d.cols_per_page, c.key - pack.row_off[t]) + f;
         store_scalar<NT>(w, sgd_apply_t<T, C, MODE>(*w, acc, eta_c, eta64));
@@ -3259,15 +3276,16 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     if (n == 0) return ET_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Exact mode (ET_FLAG_EXACT_UPDATE, and since ABI v9 ET_FLAG_EXACT_IF_FAST too: the chain
-    // path now covers every element type and gradient size): every column's gradient summed
+    // path covers every element type and gradient size): every column's gradient summed
     // serially in occurrence order, as the reference does.  Columns longer than a chunk are
-    // serial chains (k_chain_*, k_sgd_chains) whose entries hold a 24-bit bag, so a batch of
-    // 2^24 bags or more keeps every column in one chunk instead (a chunk then spans a whole
-    // segment: exact, one wave per column).
+    // serial chains (k_chain_*, k_sgd_chains) whose entries hold a 24-bit bag below 2^24 bags
+    // and a 27-bit one from there (chain_shift), so only a batch of 2^27 bags or more keeps
+    // every column in one chunk instead (a chunk then spans a whole segment: exact, one wave
+    // per column).
     const bool exact = (flags & (ET_FLAG_EXACT_UPDATE | ET_FLAG_EXACT_IF_FAST)) != 0;
     bool chain = exact;
     for (int t = 0; t < ntables && chain; ++t)
-        if (descs[t].batch >= (1 << 24)) chain = false;
+        if (descs[t].batch > et::kChainMaxBatch) chain = false;
     // chain mode: a column of at most kExactChunk occurrences is one chunk of the chunk pass
     // (a lane group's serial sum), a longer one a chain
     const uint32_t chunk = exact && !chain ? (uint32_t)(n < 0x7fffffff ? n + 1 : 0x7fffffff)

@@ -11,8 +11,14 @@ import os
 import torch  # noqa: F401  (loads torch's HIP runtime first, so the library shares it)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# ET_LIBRARY: an alternative build of the same library (the profiling builds under tools/)
+# ET_LIBRARY: an alternative build of the same library (the profiling builds under tools/).
+# An EXPERIMENT build (tools/exp_build.sh, -DET_EXPERIMENTS: it reads ET_* tuning knobs from
+# the environment and exports et_debug_chain_timeline) is refused unless the process opts in
+# with ET_TOOLS_EXPERIMENT=1, which only the scripts under tools/ set — so no environment can
+# swap a knob-reading library under the tests, smoke() or bench.py by accident.
 LIB_PATH = os.environ.get("ET_LIBRARY") or os.path.join(_HERE, "libembtab_hip.so")
+EXPERIMENT_MARKER = "et_debug_chain_timeline"
+EXPERIMENT_BUILD = False  # set by load(): the loaded library is an experiment build
 
 ET_OK = 0
 ET_F32, ET_F16, ET_F64, ET_I32, ET_I64, ET_BF16 = 0, 1, 2, 3, 4, 5
@@ -144,6 +150,13 @@ def load() -> ctypes.CDLL:
             f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
             "from the repository root (hipcc --offload-arch=gfx950)")
     L = ctypes.CDLL(LIB_PATH)
+    global EXPERIMENT_BUILD
+    EXPERIMENT_BUILD = hasattr(L, EXPERIMENT_MARKER)
+    if EXPERIMENT_BUILD and os.environ.get("ET_TOOLS_EXPERIMENT") != "1":
+        raise ImportError(
+            f"{LIB_PATH} is an experiment build of the library (it reads ET_* knobs from the "
+            "environment); the package loads it only for the tools under tools/, which set "
+            "ET_TOOLS_EXPERIMENT=1")
     vp, i64, i32, u32, u64, dbl, c_int = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                           ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
                                           ctypes.c_int)

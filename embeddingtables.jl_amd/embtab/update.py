@@ -326,7 +326,9 @@ def _sparse_sgd(descs, eta: float, flags: int, device, dtype=torch.float32):
 # src/sparseupdate.jl:110-127 — bit-identical) is the default: EXACT_DEFAULT = None passes
 # ET_FLAG_EXACT_IF_FAST, which since ABI v9 is exact for every element type and gradient size
 # (the serial-chain path: the hand-scheduled Float32 loop, or 64-bit addressed chains for a
-# gradient beyond its 32-bit offsets and for Float64 / Float16 / BFloat16 tables).
+# gradient beyond its 32-bit offsets, for a batch of 2^24 bags or more and for Float64 /
+# Float16 / BFloat16 tables).  Chains cover batches below 2^27 bags; a larger batch is still
+# exact but sums each column in one chunk (one wave per column).
 # exact=True is the same; exact=False selects the split mode (columns longer than
 # ET_SGD_CHUNK summed as ordered partial sums).
 EXACT_DEFAULT = None
@@ -345,7 +347,8 @@ def update_(*args, nontemporal: bool | None = None, exact: bool | None = None,
 
     ``exact=True`` (and the default, EXACT_DEFAULT = None) sums every column's gradient
     serially (bit-identical to the reference even for hot columns: longer columns run as
-    serial chains beside the chunk pass, for every element type and gradient size);
+    serial chains beside the chunk pass, for every element type and gradient size, batches
+    below 2^27 bags; a larger batch sums each column in one chunk, exact but slow);
     ``exact=False`` splits occurrence lists longer than ET_SGD_CHUNK (256) into partial
     sums combined in a fixed order (deterministic, not the reference's order).  Float16 tables
     use Julia's Float16 arithmetic unless ``f16_fp32_acc`` (sums in Float32).

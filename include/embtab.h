@@ -91,8 +91,11 @@ extern "C" {
 #define ET_FLAG_EXACT_IF_FAST 256u /* sparse SGD, the bindings' default: since ABI v9 the
                                     same as ET_FLAG_EXACT_UPDATE — the exact mode's serial-
                                     chain path covers every element type and gradient size
-                                    (ABI v8 resolved it to the split mode for non-Float32
-                                    tables and for batch * ld_delta >= 2^30) */
+                                    up to a batch of 2^27 - 1 bags (ABI v8 resolved it to the
+                                    split mode for non-Float32 tables and for batch *
+                                    ld_delta >= 2^30).  A batch of 2^27 bags or more is still
+                                    exact but sums every column in one chunk (one wave per
+                                    column: slow for hot columns) */
 
 /* Occurrences per chunk of the non-exact sparse SGD: a column with more occurrences than
  * this is summed as ordered partial sums of ET_SGD_CHUNK consecutive occurrences (so a

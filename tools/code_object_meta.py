@@ -21,6 +21,49 @@ MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 
 
+def _code_objects(lib: str, d: str) -> list:
+    """Paths of the gfx950 code objects unbundled from the library's .hip_fatbin into d."""
+    cos = []
+    fb = os.path.join(d, "fb.bin")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", lib,
+                    os.path.join(d, "junk")], check=True, capture_output=True)
+    data = open(fb, "rb").read()
+    starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)] + [len(data)]
+    for i in range(len(starts) - 1):
+        part = os.path.join(d, f"b{i}.bin")
+        with open(part, "wb") as f:
+            f.write(data[starts[i]:starts[i + 1]])
+        co = os.path.join(d, f"b{i}.co")
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
+                            f"--input={part}", f"--targets={TARGET}", f"--output={co}"],
+                           capture_output=True)
+        if r.returncode == 0 and os.path.getsize(co):
+            cos.append(co)
+    return cos
+
+
+def disassembly(lib: str) -> dict:
+    """{kernel symbol: its gfx950 disassembly} over every code object of the library
+    (llvm-objdump -d; a function's text runs from its `<symbol>:` line to the next one)."""
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        for co in _code_objects(lib, d):
+            text = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co],
+                                  check=True, capture_output=True, text=True).stdout
+            name, buf = None, []
+            for line in text.splitlines():
+                m = re.match(r"^[0-9a-f]+ <([^>]+)>:$", line)
+                if m:
+                    if name:
+                        out[name] = out.get(name, "") + "\n".join(buf)
+                    name, buf = m.group(1), []
+                elif name:
+                    buf.append(line)
+            if name:
+                out[name] = out.get(name, "") + "\n".join(buf)
+    return out
+
+
 def kernels(lib: str) -> list:
     """[{name, vgpr_count, agpr_count, sgpr_count, lds}] over every gfx950 code object."""
     out = []

@@ -24,6 +24,8 @@
 #   py:SCRIPT[:ARGS] python3 tools/SCRIPT ARGS (ARGS: '+'-separated)
 #   exppy:SCRIPT[:ARGS]  the same with the experiment build (tools/exp_build.sh)
 set -o pipefail
+# the package loads an experiment build (ET_LIBRARY=tools/exp/...) only with this opt-in
+export ET_TOOLS_EXPERIMENT=1
 TAG=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/$TAG
