@@ -3126,11 +3126,13 @@ inline SideStreams* side_streams() {
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
         const int n = side_stream_count();
+        // ET_SIDE_PRIO=1 (experiment builds): the side streams at the least priority
+        const int prio = ET_KNOB("ET_SIDE_PRIO", 0) ? least : greatest;
         for (int i = 0; i < n; ++i)
             if ((!ss.fork[i] && hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming)) ||
                 (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
                 (!ss.st[i] &&
-                 hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking, greatest)))
+                 hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking, prio)))
                 return nullptr;
         // acquire the hardware queues now, back to back (an event record is a packet on the
         // stream's queue)

@@ -267,8 +267,10 @@ const QUEUE = Ref{Any}(nothing)
 function _queue_block()
     if QUEUE[] === nothing
         q = HipArray{UInt8}(undef, ET_LOOKUP_QUEUE_BYTES)
-        ccall((:hipMemset, libhip), Cint, (Ptr{Cvoid}, Cint, Csize_t), q.ptr, 0,
-              ET_LOOKUP_QUEUE_BYTES) == 0 || error("hipMemset failed")
+        # zeroed on stream(), so the first et_maplookup_prealloc_q on that stream (blocking or
+        # not) sees a zero block
+        ccall((:hipMemsetAsync, libhip), Cint, (Ptr{Cvoid}, Cint, Csize_t, Ptr{Cvoid}), q.ptr, 0,
+              ET_LOOKUP_QUEUE_BYTES, stream()) == 0 || error("hipMemsetAsync failed")
         QUEUE[] = q
     end
     return QUEUE[].ptr
@@ -388,29 +390,69 @@ mutable struct HipIndexer <: AbstractIndexer
     map::Union{Nothing,HipVector{Int64}}             # gradient column of each occurrence
     nunique_dev::Union{Nothing,HipVector{Int64}}
     workspace::Union{Nothing,HipVector{UInt8}}
+    # the index array a multi-table update!'s index phase copied (et_sparse_sgd_snap) and its
+    # (pool, batch, maxindex) while not yet indexed: built into the fields above on first read
+    snapshot::Union{Nothing,HipVector{Int64}}
+    pending::Union{Nothing,NTuple{3,Int}}
 end
-HipIndexer() = HipIndexer(nothing, nothing, nothing, nothing, nothing)
+HipIndexer() = HipIndexer(nothing, nothing, nothing, nothing, nothing, nothing, nothing)
 
-# index!(indexer, A, maxindex) (src/utils.jl:306-314) on the device, stream-ordered.
-function index!(ix::HipIndexer, I::Union{HipVector{Int},HipMatrix{Int}}, maxindex)
+# Reading any Indexer field first indexes a pending snapshot (stream-ordered after the
+# update that wrote it), as the Python host's Indexer._defer / _materialise.
+const _INDEXER_FIELDS = (:cumulative_col, :cumulative_off, :map, :nunique_dev)
+function Base.getproperty(ix::HipIndexer, s::Symbol)
+    s in _INDEXER_FIELDS && _materialise!(ix)
+    return getfield(ix, s)
+end
+
+function _materialise!(ix::HipIndexer)
+    p = getfield(ix, :pending)
+    p === nothing && return ix
+    setfield!(ix, :pending, nothing)
+    pool, batch, maxindex = p
+    return _index_build!(ix, getfield(ix, :snapshot).ptr, pool, batch, maxindex)
+end
+
+# The snapshot buffer a multi-table update! hands to et_sparse_sgd_snap for this Indexer
+# (contiguous pool x batch; reused while unread or large enough).
+function _snapshot!(ix::HipIndexer, I::Union{HipVector{Int},HipMatrix{Int}}, maxindex)
     pool = ndims(I) == 1 ? 1 : size(I, 1)
     batch = size(I, ndims(I))
+    buf = getfield(ix, :snapshot)
+    if buf === nothing || length(buf) < pool * batch
+        buf = HipArray{Int64}(undef, max(pool * batch, 1))
+        setfield!(ix, :snapshot, buf)
+    end
+    setfield!(ix, :pending, (pool, batch, Int(maxindex)))
+    return buf.ptr
+end
+
+function _index_build!(ix::HipIndexer, idx::Ptr{Int64}, pool, batch, maxindex)
     n = pool * batch
-    if ix.map === nothing || length(ix.map) < max(n, 1)
-        ix.cumulative_col = HipArray{Int64}(undef, n + 1)
-        ix.cumulative_off = HipArray{Int64}(undef, n + 1)
-        ix.map = HipArray{Int64}(undef, max(n, 1))
-        ix.nunique_dev = HipArray{Int64}(undef, 1)
+    if getfield(ix, :map) === nothing || length(getfield(ix, :map)) < max(n, 1)
+        setfield!(ix, :cumulative_col, HipArray{Int64}(undef, n + 1))
+        setfield!(ix, :cumulative_off, HipArray{Int64}(undef, n + 1))
+        setfield!(ix, :map, HipArray{Int64}(undef, max(n, 1)))
+        setfield!(ix, :nunique_dev, HipArray{Int64}(undef, 1))
         nb = Ref{Int64}(0)
         check(ccall((:et_index_workspace_size, libembtab), Cint, (Int64, Ref{Int64}), n, nb))
-        ix.workspace = HipArray{UInt8}(undef, nb[])
+        setfield!(ix, :workspace, HipArray{UInt8}(undef, nb[]))
     end
+    ws = getfield(ix, :workspace)
     check(ccall((:et_index_build, libembtab), Cint,
                 (Ptr{Int64}, Int32, Int64, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Int64},
                  Ptr{Int64}, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
-                I.ptr, pool, pool, batch, maxindex, ix.cumulative_col.ptr, ix.cumulative_off.ptr,
-                ix.map.ptr, ix.nunique_dev.ptr, ix.workspace.ptr, length(ix.workspace), stream()))
+                idx, pool, pool, batch, maxindex, getfield(ix, :cumulative_col).ptr,
+                getfield(ix, :cumulative_off).ptr, getfield(ix, :map).ptr,
+                getfield(ix, :nunique_dev).ptr, ws.ptr, length(ws), stream()))
     return ix
+end
+
+# index!(indexer, A, maxindex) (src/utils.jl:306-314) on the device, stream-ordered.
+function index!(ix::HipIndexer, I::Union{HipVector{Int},HipMatrix{Int}}, maxindex)
+    setfield!(ix, :pending, nothing)  # an explicit index! replaces an unread snapshot
+    pool = ndims(I) == 1 ? 1 : size(I, 1)
+    return _index_build!(ix, pointer(I), pool, size(I, ndims(I)), maxindex)
 end
 nunique(ix::HipIndexer) = download(ix.nunique_dev)[1]
 
@@ -434,19 +476,29 @@ end
 # src/sparseupdate.jl:199-238: index all tables, telemetry_cb(), update all tables.
 # One device pipeline per (path, eltype) group, split at the same boundary
 # (ET_FLAG_SGD_INDEX_ONLY, then ET_FLAG_SGD_APPLY_ONLY from the same workspace);
-# telemetry_cb (if given) runs once the index phase is enqueued.  indexers[i] receives table i's
-# Indexer in the index phase as the reference's does: a HipIndexer is built on the device
-# (et_index_build, stream-ordered, no host work).  A host Indexer is filled by the
-# reference's own serial index! on a downloaded copy of the indices only when asked for
-# (fill_host_indexers = true): that costs a PCIe copy of every index array and a host
-# pass over every occurrence per step (272 MB and 34 M insertions at BASELINE config 4).
+# telemetry_cb (if given) runs once the index phase is enqueued.  indexers[i] is filled in
+# the index phase, as the reference's (:210-213):
+#  * a HipIndexer receives a SNAPSHOT of grads[i].indices written by the update's own key pass
+#    (et_sparse_sgd_snap: 8 bytes per occurrence beside the keys, no separate pass and no
+#    second sort), indexed on the device (et_index_build) when it is first read — so a caller
+#    that refills the index buffer before reading indexers[i] still gets this update's;
+#  * a host Indexer (the reference's own type) is filled by the reference's serial index! on a
+#    downloaded copy of the indices (fill_host_indexers = true, the default, as the reference
+#    does; false skips it: a PCIe copy of every index array and a host pass over every
+#    occurrence per step, 272 MB and 34 M insertions at BASELINE config 4).
+# One Indexer object at several positions ends up holding the LAST one's indices, as the
+# reference's sequential index! calls leave it, so only its last position is snapshotted.
 const WORKSPACES = Dict{Int,Any}()
 function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  grads::AbstractVector{<:SparseEmbeddingUpdate},
                  indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
-                 telemetry_cb = nothing, fill_host_indexers::Bool = false,
+                 telemetry_cb = nothing, fill_host_indexers::Bool = true,
                  exact::Union{Nothing,Bool} = EXACT[], kw...) where {Nontemporal}
     nt = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) | _exact_flag(exact)
+    lastpos = IdDict{Any,Int}(ix => i for (i, ix) in pairs(indexers))
+    snap = [indexers[i] isa HipIndexer && lastpos[indexers[i]] == i && !isempty(grads[i].indices) ?
+            _snapshot!(indexers[i], grads[i].indices, size(tables[i], 2)) : Ptr{Int64}(C_NULL)
+            for i in eachindex(indexers, grads)]
     calls = []
     for fused in (true, false), T in (Float32, Float64, Float16)
         sel = [i for i in eachindex(tables) if _fused(tables[i]) == fused &&
@@ -465,29 +517,36 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                 ws = HipArray{UInt8}(undef, nb[])
                 WORKSPACES[k] = ws
             end
-            push!(calls, (T, descs, flags, ws))
+            push!(calls, (T, descs, flags, ws, Ptr{Int64}[snap[i] for i in chunk]))
         end
     end
-    run(phase) = for (T, descs, flags, ws) in calls
+    # phase 1 (or the whole update): the snapshots ride in the key pass
+    index_phase(phase) = for (T, descs, flags, ws, snaps) in calls
+        check(ccall((:et_sparse_sgd_snap, libembtab), Cint,
+                    (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Ptr{Int64}}, Ptr{Cvoid},
+                     Int64, Ptr{Cvoid}),
+                    et_dtype(T), descs, length(descs), Float64(opt.eta), flags | phase, snaps,
+                    ws.ptr, length(ws), stream()))
+    end
+    apply_phase() = for (T, descs, flags, ws, _) in calls
         check(ccall((:et_sparse_sgd, libembtab), Cint,
                     (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
-                    et_dtype(T), descs, length(descs), Float64(opt.eta), flags | phase, ws.ptr,
-                    length(ws), stream()))
+                    et_dtype(T), descs, length(descs), Float64(opt.eta),
+                    flags | ET_FLAG_SGD_APPLY_ONLY, ws.ptr, length(ws), stream()))
     end
     # without a callback nothing observes the phase boundary: one call per group (the
     # same device work and order; exact mode's early chains start with the call)
     phased = telemetry_cb !== nothing
-    run(phased ? ET_FLAG_SGD_INDEX_ONLY : UInt32(0))
-    for i in eachindex(indexers, grads)
-        if indexers[i] isa HipIndexer
-            index!(indexers[i], grads[i].indices, size(tables[i], 2))
-        elseif fill_host_indexers
+    index_phase(phased ? ET_FLAG_SGD_INDEX_ONLY : UInt32(0))
+    if fill_host_indexers
+        for i in eachindex(indexers, grads)
+            indexers[i] isa HipIndexer && continue
             EmbeddingTables.index!(indexers[i], download(grads[i].indices), size(tables[i], 2))
         end
     end
     if phased
         telemetry_cb()
-        run(ET_FLAG_SGD_APPLY_ONLY)
+        apply_phase()
     end
     return nothing
 end

@@ -141,14 +141,45 @@ def test_shim_structs_match_the_header():
         assert jf == hs[c], (jl, jf, hs[c])
 
 
-def test_multi_table_update_does_no_host_indexing_by_default():
+def _multi_table_update_body() -> str:
     src = open(SHIM).read()
     m = re.search(r"function update!\(opt::Flux\.Descent, tables::AbstractVector.*?^end", src,
                   re.S | re.M)
     assert m, "multi-table update! not found"
-    body = m.group(0)
-    assert "fill_host_indexers::Bool = false" in body
-    # the host index! (on downloaded indices) runs only under the opt-in flag
+    return m.group(0)
+
+
+def test_multi_table_update_snapshots_through_et_sparse_sgd_snap():
+    """the multi-table update! fills indexers[i] in its index phase as the
+    reference does (src/sparseupdate.jl:210-213) and as the Python host does
+    (embtab/update.py: Indexer._defer + et_sparse_sgd_snap): the snapshots ride in the update's
+    own key pass, and no second sort (et_index_build / index!) runs on that path — a
+    HipIndexer is indexed from its snapshot only when first read."""
+    body = _multi_table_update_body()
+    decl = header_functions()
+    calls = [c for c in shim_ccalls() if c[0] == "et_sparse_sgd_snap"]
+    assert calls, "the shim never binds et_sparse_sgd_snap"
+    for name, ret, args in calls:  # the header's signature
+        assert [jl_class(a) for a in args] == decl[name][1] and ret == "Cint"
+    assert re.search(r"ccall\(\(:et_sparse_sgd_snap, libembtab\)", body)
+    # the snapshot pointers handed to it are the HipIndexers' (last position of each object)
+    assert "_snapshot!(indexers[i], grads[i].indices" in body
+    # no second device sort per HipIndexer on this path
+    assert "et_index_build" not in body and "index!(indexers[i], grads[i]" not in body
+    code = re.sub(r"#.*", "", body)
+    assert not re.search(r"(?<![.\w])index!\(", code)
+    # the deferred build: reading a HipIndexer field materialises a pending snapshot
+    src = open(SHIM).read()
+    assert re.search(r"function Base\.getproperty\(ix::HipIndexer", src)
+    assert "_materialise!(ix)" in src
+
+
+def test_multi_table_update_fills_host_indexers_by_default():
+    """A host Indexer (the reference's type) is filled by the reference's own index! by
+    default, as the reference's index phase fills every indexers[i]; the flag turns it off."""
+    body = _multi_table_update_body()
+    assert "fill_host_indexers::Bool = true" in body
     host = body.index("EmbeddingTables.index!(")
-    assert body.rfind("elseif fill_host_indexers", 0, host) != -1
-    assert "HipIndexer" in body  # device indexers are filled on the device
+    assert body.rfind("if fill_host_indexers", 0, host) != -1
+    # before the telemetry callback and the apply phase (the reference's phase order)
+    assert host < body.index("telemetry_cb()") < body.index("apply_phase()", host)
