@@ -414,7 +414,11 @@ __device__ __forceinline__ uint64_t row_off_s(int64_t v, uint32_t ldb, uint32_t 
 // One batch of UU rows of both bags.  Returns false — before issuing any row load —
 // if an index of the batch is out of range; the caller then redoes the bag pair with
 // bag_pair_checked.
-template <typename T, typename A, int UU, bool NTL, int BPL = 16>
+// NA (experiment builds only, ET_HEAD_NOADD): the same loads, waits and stores with the adds
+// replaced by an empty consumer (each loaded vector is an input of an empty asm, so its
+// load must complete there; the result is the bag's first row, not its sum) — the ceiling of
+// this schedule's byte mix without the arithmetic.
+template <typename T, typename A, int UU, bool NTL, int BPL = 16, int NA = 0>
 __device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t nrows,
                                            cidx_ptr ia, cidx_ptr ib, uint64_t hmask,
                                            uint64_t lane_off, bool first_batch,
@@ -447,6 +451,15 @@ __device__ __forceinline__ bool load_add_s(uintptr_t tb, uint32_t ldb, uint32_t 
     for (int u = 0; u < UU; ++u) {
         T x[N];
         __builtin_memcpy(x, &buf[u], BPL);
+        if constexpr (NA != 0) {
+            if (u == 0 && first_batch) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k] = A(x[k]);
+            } else {
+                asm volatile("" ::"v"(buf[u]));
+            }
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < N; ++k) {
             if (u == 0)
@@ -483,7 +496,7 @@ __device__ __forceinline__ void bag_pair_checked(uintptr_t tb, uint32_t ldb, uin
 
 // `rounds` rounds of 8 bags per workgroup (bag mapping identical to run_bags: wave w
 // of round r holds bags chunk*8*rounds + r*8 + 2w + {0, 1}).
-template <typename T, typename A, int U, bool NT, bool NTL, int BPL = 16>
+template <typename T, typename A, int U, bool NT, bool NTL, int BPL = 16, int NA = 0>
 __device__ __forceinline__ void run_bags_s(const et_lookup_desc& d, int64_t batch,
                                            T* __restrict__ dst, int64_t ld_dst, int64_t chunk,
                                            int rounds) {
@@ -511,7 +524,7 @@ __device__ __forceinline__ void run_bags_s(const et_lookup_desc& d, int64_t batc
         bool ok = true;
         int i0 = 0;
 #define ET_LOAD_ADD_S(UU) \
-    load_add_s<T, A, UU, NTL, BPL>(tb, ldb, nr, ia + i0, ib + i0, hmask, lane_off, i0 == 0, acc)
+    load_add_s<T, A, UU, NTL, BPL, NA>(tb, ldb, nr, ia + i0, ib + i0, hmask, lane_off, i0 == 0, acc)
         for (; ok && i0 + U <= pool; i0 += U) ok = ET_LOAD_ADD_S(U);
         if constexpr (U > 4) {
             if (ok && pool - i0 >= 4) {
@@ -589,7 +602,7 @@ struct StripeMap {
     int qorder;            // queued schedule: 1 = every heavy item before the light ones
 };
 
-template <typename T, typename A, int D, int U, bool NT, bool NTI, bool SG = false>
+template <typename T, typename A, int D, int U, bool NT, bool NTI, bool SG = false, int NA = 0>
 __device__ __forceinline__ void striped_body(const LookupPack& pack, const StripeMap& sm,
                                              int ntables, int64_t batch, T* __restrict__ dst,
                                              int64_t ld_dst, int rounds, int64_t stripe_chunks,
@@ -635,11 +648,11 @@ __device__ __forceinline__ void striped_body(const LookupPack& pack, const Strip
 #endif
     if constexpr (SG) {
         if ((sm.ntload_mask >> t) & 1u)
-            run_bags_s<T, A, U, NT, true, sg_bpl<T>(D)>(pack.d[t], batch, dst, ld_dst, chunk,
-                                                         rounds);
+            run_bags_s<T, A, U, NT, true, sg_bpl<T>(D), NA>(pack.d[t], batch, dst, ld_dst, chunk,
+                                                             rounds);
         else
-            run_bags_s<T, A, U, NT, false, sg_bpl<T>(D)>(pack.d[t], batch, dst, ld_dst, chunk,
-                                                          rounds);
+            run_bags_s<T, A, U, NT, false, sg_bpl<T>(D), NA>(pack.d[t], batch, dst, ld_dst, chunk,
+                                                              rounds);
     } else {
         if ((sm.ntload_mask >> t) & 1u)
             run_bags<T, A, D, U, NT, true, NTI>(pack.d[t], batch, dst, ld_dst, chunk, rounds);
@@ -708,7 +721,7 @@ struct XcdQueue {
 };
 static_assert(sizeof(XcdQueue) == ET_LOOKUP_QUEUE_BYTES, "queue block size (include/embtab.h)");
 
-template <typename T, typename A, int D, int U, bool NT, bool SG>
+template <typename T, typename A, int D, int U, bool NT, bool SG, int NA = 0>
 __global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, StripeMap sm,
                                                            int ntables, int64_t batch,
                                                            T* __restrict__ dst, int64_t ld_dst,
@@ -750,8 +763,8 @@ __global__ __launch_bounds__(256) void k_pooled_vec_queued(LookupPack pack, Stri
                              : ((slot - ln) / sm.nheavy) * ntables + (slot - ln) % sm.nheavy;
         }
 #endif
-        striped_body<T, A, D, U, NT, false, SG>(pack, sm, ntables, batch, dst, ld_dst, rounds,
-                                                stripe_chunks, nchunks, (int)(it / per), slot);
+        striped_body<T, A, D, U, NT, false, SG, NA>(pack, sm, ntables, batch, dst, ld_dst, rounds,
+                                                    stripe_chunks, nchunks, (int)(it / per), slot);
     }
     if (threadIdx.x == 0 && atomicAdd(&q.done, 1u) == gridDim.x - 1u) {  // the last one
         for (int x = 0; x < kXcds; ++x) atomicExch(&q.head[x], 0u);
@@ -1016,6 +1029,7 @@ struct LookupTuning {
     int sg256 = 0;                 // ET_SG256=1: 256-byte rows take the scalar loop too
     int heavy_prio = 0;            // ET_HEAVY_PRIO=1: heavy tables' waves at priority 2
     int qorder = 0;                // ET_QORDER=1: queued schedule, heavy items first
+    int noadd = 0;                 // ET_HEAD_NOADD=1: the scalar loop without its adds
     // Tables of (light_bytes, fsplit_bytes] cut into fsplit_g feature groups, group g on XCDs
     // [g * 8 / G, (g + 1) * 8 / G), so each XCD's L2 holds 1/G of the table (ET_FSPLIT_*)
     int64_t fsplit_bytes = 0;
@@ -1038,6 +1052,7 @@ inline const LookupTuning& tuning() {
         v.light_bytes = ET_KNOB("ET_LIGHT_BYTES", v.light_bytes);
         v.rows_in_flight = (int)ET_KNOB("ET_U", v.rows_in_flight);
         v.w8 = (int)ET_KNOB("ET_W8", v.w8);
+        v.noadd = (int)ET_KNOB("ET_HEAD_NOADD", v.noadd);
         v.sgpr = (int)ET_KNOB("ET_SGPR", v.sgpr);
         v.sg256 = (int)ET_KNOB("ET_SG256", v.sg256);
         v.heavy_prio = (int)ET_KNOB("ET_HEAVY_PRIO", v.heavy_prio);
@@ -1158,6 +1173,16 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
         if (grid > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
         if (pack.queue && tuning().queued && grid < 0xffffffffll) {
             if constexpr (kSG) {
+#ifdef ET_EXPERIMENTS
+                if (sg && tuning().noadd) {  // ET_HEAD_NOADD: the adds-free ceiling variant
+                    hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, true, 1>),
+                                       dim3((unsigned)grid), dim3(256), 0, s, pack, sm, ne, batch,
+                                       reinterpret_cast<T*>(dst), ld_dst, rounds, stripe_chunks,
+                                       nchunks);
+                    ET_LAUNCH_CHECK("k_pooled_vec_queued<noadd>");
+                    return ET_OK;
+                }
+#endif
                 if (sg) {
                     hipLaunchKernelGGL((k_pooled_vec_queued<T, A, D, U, NT, true>),
                                        dim3((unsigned)grid), dim3(256), 0, s, pack, sm, ne, batch,
@@ -1556,7 +1581,6 @@ extern "C" int et_gather(int dtype, const void* table, int64_t ld_table, int64_t
                          int32_t dim, const int64_t* idx, int64_t n, void* dst, int64_t ld_dst,
                          uint32_t flags, void* stream) {
     et::clear_err();
-    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (dim > 0 && ld_dst < dim) return et::fail(ET_ERR_ARG, "ld_dst < dim");
     et_lookup_desc d;
     d.table = table;
@@ -1578,7 +1602,6 @@ extern "C" int et_pooled_sum(int dtype, const void* table, int64_t ld_table, int
                              int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                              void* stream) {
     et::clear_err();
-    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (dim > 0 && ld_dst < dim) return et::fail(ET_ERR_ARG, "ld_dst < dim");
     // pool == 0: the sum over an empty bag is zero(T); the generic kernel writes zeros.
     et_lookup_desc d;
@@ -1601,7 +1624,6 @@ extern "C" int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int
                                      int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                                      void* stream) {
     et::clear_err();
-    et::open_side_streams(static_cast<hipStream_t>(stream));
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Empty bags (pool == 0) are handled by the generic kernel, which writes zeros.
     // f16 pool == 1 tables are bit copies; the flag only matters for pool >= 2, where the
@@ -1613,7 +1635,6 @@ extern "C" int et_maplookup_prealloc_q(int dtype, const et_lookup_desc* descs, i
                                        int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                                        void* queue, void* stream) {
     et::clear_err();
-    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (queue && (reinterpret_cast<uintptr_t>(queue) & 15u))
         return et::fail(ET_ERR_ARG, "queue block is not 16-byte aligned");
     return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags,
@@ -1624,7 +1645,6 @@ extern "C" int et_maplookup_prealloc_to(int dtype, int dst_dtype, const et_looku
                                         int32_t ntables, int64_t batch, void* dst,
                                         int64_t ld_dst, uint32_t flags, void* stream) {
     et::clear_err();
-    et::open_side_streams(static_cast<hipStream_t>(stream));
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (dst_dtype == dtype)
         return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags, s);

@@ -220,20 +220,26 @@ def maplookup_(strategy: AbstractExecutionStrategy, dst, tables, I, nontemporal:
 # Queue blocks of the per-XCD work-queue schedule (et_maplookup_prealloc_q), one per
 # (device, stream, thread): calls that share a block are ordered by their stream.  Zeroed once
 # on that stream when made; every launch leaves its block zero again.
-_QUEUE_BLOCKS: dict = {}
+# one block per (device, stream handle) PER THREAD, in thread-local storage: two threads never
+# share a block, and a thread's blocks are freed when it exits
+_QUEUE_BLOCKS = threading.local()
 
 
 def _queue_block(device: torch.device, stream: int):
     """The queue block for launches on `stream`, or None while the stream is capturing a
     HIP graph (the captured launch keeps the static stripe schedule: a block allocated
     during a capture would be graph-private memory)."""
-    if torch.cuda.is_current_stream_capturing():
-        return None
-    key = (device.index, stream, threading.get_ident())
-    q = _QUEUE_BLOCKS.get(key)
+    with torch.cuda.device(device):  # the capture state of THIS device's current stream
+        if torch.cuda.is_current_stream_capturing():
+            return None
+    blocks = getattr(_QUEUE_BLOCKS, "d", None)
+    if blocks is None:
+        blocks = _QUEUE_BLOCKS.d = {}
+    key = (device.index, stream)
+    q = blocks.get(key)
     if q is None:
         q = torch.zeros(_lib.ET_LOOKUP_QUEUE_BYTES // 4, dtype=torch.int32, device=device)
-        _QUEUE_BLOCKS[key] = q
+        blocks[key] = q
     return q
 
 

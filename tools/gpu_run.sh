@@ -88,18 +88,22 @@ print('bench', round(d['ms_per_step'],4), 'ms frac', round(d['roofline']['frac']
           -- python3 tools/exact_cfg4.py exact > "$D/$grp.log" 2>&1 || die "updpmc $grp" "$D/$grp.log"
       done
       python3 tools/kernel_traffic.py "$D" > "$D/per_kernel.txt" && head -25 "$D/per_kernel.txt" ;;
-    classpmc)
+    classpmc|expclasspmc:*)
+      # expclasspmc:VAR=V,..: the same passes with the experiment build and env VAR=V
+      SETS=""; LIBV=""; CD=classpmc
+      if [ "$step" != classpmc ]; then SETS=${step#expclasspmc:}; LIBV=$EXP; CD=classpmc_exp; fi
       for c in heavy mid light all; do
-        D=$OUT/classpmc/$c; mkdir -p "$D"
-        timeout -k 10 120 python3 tools/class_pmc.py $c 10 > "$D/time.json" 2> "$D/time.err" || die classpmc "$D/time.err"
+        D=$OUT/$CD/$c; mkdir -p "$D"
+        env ET_LIBRARY=$LIBV $(echo "$SETS" | tr ',' ' ') timeout -k 10 120 python3 tools/class_pmc.py $c 10 \
+          > "$D/time.json" 2> "$D/time.err" || die classpmc "$D/time.err"
         for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
           tag=$(echo "$grp" | tr ' ' '_')
-          timeout -s KILL 100 rocprofv3 --pmc $grp -d "$D/$tag" -o run --output-format csv \
+          env ET_LIBRARY=$LIBV $(echo "$SETS" | tr ',' ' ') timeout -s KILL 100 rocprofv3 --pmc $grp -d "$D/$tag" -o run --output-format csv \
             -- python3 tools/class_pmc.py $c 5 > "$D/$tag.log" 2>&1 || die "classpmc $c $tag" "$D/$tag.log"
         done
         python3 tools/traffic.py "$D" k_pooled_vec "class_$c" "$D/traffic.json" > /dev/null
         python3 -c "import json; t=json.load(open('$D/time.json')); d=json.load(open('$D/traffic.json')); \
-print('$c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric', round(d.get('hbm_bytes_per_launch',0)/1e9,3), 'GB', \
+print('$SETS $c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric', round(d.get('hbm_bytes_per_launch',0)/1e9,3), 'GB', \
 'compulsory', round(t['hbm_compulsory_bytes']/1e9,3), 'GB', 'alg', round(t['algorithmic_bytes']/1e9,3), 'GB', 'L2hit', round(d.get('l2_hit_rate',0),3))"
       done ;;
     cfg2)
@@ -168,6 +172,16 @@ print('$c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric', roun
         timeout -k 10 240 python3 tools/capture_effect.py "$m" 10 >> "$OUT/capture_modes.jsonl" 2> "$OUT/capture_$m.err" \
           || die "capture $m" "$OUT/capture_$m.err"
         tail -1 "$OUT/capture_modes.jsonl"
+      done ;;
+    qmap:*)
+      # kernel trace of the update after each capture_effect mode: queue / stream / duration
+      for m in $(echo "${step#qmap:}" | tr ',' ' '); do
+        timeout -k 10 240 rocprofv3 --kernel-trace -d "$OUT/qmap_$m" -o run --output-format csv \
+          -- python3 tools/capture_effect.py "$m" 5 > "$OUT/qmap_$m.json" 2> "$OUT/qmap_$m.err" \
+          || die "qmap $m" "$OUT/qmap_$m.err"
+        f=$(ls "$OUT"/qmap_$m/*/run_kernel_trace.csv "$OUT"/qmap_$m/run_kernel_trace.csv 2>/dev/null | head -1)
+        python3 tools/queue_map.py "$f" > "$OUT/qmap_$m.txt" && rm -rf "$OUT/qmap_$m"
+        echo "$m $(tail -1 "$OUT/qmap_$m.json")"
       done ;;
     expcapture:*)
       IFS=: read -r _ SETS MODES <<< "$step"
