@@ -447,9 +447,7 @@ def bench_config4(et, tables, tids, device, steps, warmup, batch):
     # the early chains start with the update call, so that ordering measured 6.49-6.60 ms
     # against 5.22-5.46 serial in rounds 3-4)
     fwd_ms = _timed(fwd, steps, warmup, stream)
-    # >= 6 warm-up calls: the library learns which of its four side queues to leave out from
-    # the first five full calls of a caller stream (et_update.hip SideStreams)
-    upd_ms = _timed(upd, steps, max(warmup, 6), stream)
+    upd_ms = _timed(upd, steps, warmup, stream)
     step_ms = _timed(step, steps, warmup, stream)
     # the other update mode, and how far the split mode lies from the exact (reference-
     # order, src/sparseupdate.jl:110-127) result: both from the same tables, every element

@@ -89,6 +89,10 @@ inline long long env_knob(const char* name, long long dflt) {
 // through ET_OOB_READER and et_check_errors sums them.
 static __device__ unsigned long long g_oob_count;
 
+// Opens the device's exact-update side queues at the first library call (et_update.hip,
+// SideStreams: the order in which a process opens hardware queues decides their pipes).
+void open_side_streams(hipStream_t caller);
+
 int oob_take_lookup(uint64_t* v);
 int oob_take_update(uint64_t* v);
 int oob_take_misc(uint64_t* v);

@@ -1581,6 +1581,7 @@ extern "C" int et_gather(int dtype, const void* table, int64_t ld_table, int64_t
                          int32_t dim, const int64_t* idx, int64_t n, void* dst, int64_t ld_dst,
                          uint32_t flags, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (dim > 0 && ld_dst < dim) return et::fail(ET_ERR_ARG, "ld_dst < dim");
     et_lookup_desc d;
     d.table = table;
@@ -1602,6 +1603,7 @@ extern "C" int et_pooled_sum(int dtype, const void* table, int64_t ld_table, int
                              int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                              void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (dim > 0 && ld_dst < dim) return et::fail(ET_ERR_ARG, "ld_dst < dim");
     // pool == 0: the sum over an empty bag is zero(T); the generic kernel writes zeros.
     et_lookup_desc d;
@@ -1624,6 +1626,7 @@ extern "C" int et_maplookup_prealloc(int dtype, const et_lookup_desc* descs, int
                                      int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                                      void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     hipStream_t s = static_cast<hipStream_t>(stream);
     // Empty bags (pool == 0) are handled by the generic kernel, which writes zeros.
     // f16 pool == 1 tables are bit copies; the flag only matters for pool >= 2, where the
@@ -1635,6 +1638,7 @@ extern "C" int et_maplookup_prealloc_q(int dtype, const et_lookup_desc* descs, i
                                        int64_t batch, void* dst, int64_t ld_dst, uint32_t flags,
                                        void* queue, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (queue && (reinterpret_cast<uintptr_t>(queue) & 15u))
         return et::fail(ET_ERR_ARG, "queue block is not 16-byte aligned");
     return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags,
@@ -1645,6 +1649,7 @@ extern "C" int et_maplookup_prealloc_to(int dtype, int dst_dtype, const et_looku
                                         int32_t ntables, int64_t batch, void* dst,
                                         int64_t ld_dst, uint32_t flags, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (dst_dtype == dtype)
         return et::lookup_dispatch(dtype, descs, ntables, batch, dst, ld_dst, flags, s);

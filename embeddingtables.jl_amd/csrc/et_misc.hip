@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void k_push_cols(const char* __restrict__ src,
 extern "C" int et_push_cols(int dtype, const void* src, int64_t ld, int64_t batch, int64_t col,
                             int64_t ncols, void* const* peers, int32_t npeers, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     const int es = et::elsize(dtype);
     if (!es) return et::fail(ET_ERR_UNSUPPORTED, "dtype %d", dtype);
     if (npeers < 0 || npeers > ET_MAX_PEERS)
@@ -196,6 +197,7 @@ extern "C" const char* et_last_error(void) { return et::err_buf(); }
 extern "C" int et_fill_uniform(int dtype, void* dst, int64_t n, uint64_t seed, uint64_t offset,
                                double lo, double hi, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (n < 0) return et::fail(ET_ERR_ARG, "negative n");
     if (n == 0) return ET_OK;
     if (!dst) return et::fail(ET_ERR_ARG, "dst is NULL");
@@ -237,6 +239,7 @@ extern "C" int et_fill_uniform(int dtype, void* dst, int64_t n, uint64_t seed, u
 extern "C" int et_fill_index_uniform(int64_t* idx, int64_t n, int64_t nrows, uint64_t seed,
                                      uint64_t offset, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (n < 0 || nrows <= 0) return et::fail(ET_ERR_ARG, "need n >= 0 and nrows > 0");
     if (n == 0) return ET_OK;
     if (!idx) return et::fail(ET_ERR_ARG, "idx is NULL");
@@ -252,6 +255,7 @@ extern "C" int et_concat_slabs(int dtype, const void* slabs, int32_t nranks, int
                                int64_t batch, const int32_t* rows, const int64_t* dst_row_off,
                                void* dst, int64_t ld_dst, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     return et::slab_copy<false>(dtype, const_cast<void*>(slabs), nranks, slab_ld, batch, rows,
                                 dst_row_off, dst, ld_dst, stream);
 }
@@ -260,6 +264,7 @@ extern "C" int et_split_slabs(int dtype, const void* src, int64_t ld_src, int64_
                               int32_t nranks, const int32_t* rows, const int64_t* src_row_off,
                               void* slabs, int64_t slab_ld, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     return et::slab_copy<true>(dtype, slabs, nranks, slab_ld, batch, rows, src_row_off,
                                const_cast<void*>(src), ld_src, stream);
 }

@@ -3084,49 +3084,47 @@ constexpr uint32_t kExactChunk = ET_SGD_CHUNK;
 // shared, so a call that uses the side streams holds `mu` from its first fork to its last
 // join.
 //
-// Which hardware queues the side streams get matters.  A
-// process's hardware queues are spread over the command processor's pipes in the order they
-// are opened (queue i on pipe (i - 1) mod 4 fits every measurement: profiles/r05/capture/,
-// profiles/r06/queue_layout/), and a queue that shares a pipe with the caller's queue slows
-// the caller's dispatches 2-4x (the index phase's short kernels: scans 11 -> 42 us,
-// k_build_keys 128 -> 235 us): the config-4 update took 4.7-4.8 ms instead of 3.7 whenever a
-// program had opened one or two streams, or captured a graph, before its first update
-// (tools/capture_effect.py first1 / first2).  Which pipe a queue lands on cannot be read
-// (HW_REG_HW_ID's pipe field names the XCC-local dispatch path, not the queue's pipe:
-// tools/microbench/hwid_probe.hip), and round 5's remedy — open the side queues at the
-// library's first call of any entry point — fails for exactly those programs.
+// When the side queues are opened matters.  A process's hardware queues
+// are spread over the command processor's pipes in the order they are opened (queue i on
+// pipe (i - 1) mod 4 fits every measurement below), and a queue that shares a pipe with a
+// queue holding a long-running kernel or a blocked barrier (a stream wait) dispatches its
+// own kernels 2-4x more slowly.  Round 4 opened the side queues at the first exact update:
+// the caller's queue is usually the process's first, so the three side queues took the three
+// other pipes — unless the process had opened other queues in between (a torch.cuda.graph
+// capture, or ANY stream that ran a kernel: tools/capture_effect.py), which put one side
+// queue on the caller's pipe: the index phase's kernels ran 2-4x longer and the config-4
+// update took 5.1-5.3 ms instead of 4.03-4.07 (profiles/r05/capture/).  Moving all of the
+// call's work to library streams (the caller's queue then holds only the join barriers) was
+// tried: 4.15-4.29 ms with other queues open, 4.63-4.69 ms without (the work queue then
+// shares the caller's pipe and its blocked join barrier; ET_WORK_STREAM=1 in experiment
+// builds, profiles/r05/queue_layout.txt).  So the caller's stream keeps the work, and the
+// side queues are opened at the FIRST call into the library on the device, of any entry
+// point (et::open_side_streams(), from every stream-taking ABI function), right after the
+// caller's own queue, before most programs open other streams; init() touches each with an
+// event record, which acquires its hardware queue.
 //
-// So the library opens FOUR side streams back to back (four consecutive queues: one per pipe)
-// and uses three of them; the one it leaves out is learned per caller stream from the calls
-// themselves (SidePick): after one warm-up call, each of the four choices times one full
-// update call (events on the caller's stream around the call), then the fastest is kept.
-// Every choice gives the same results (the streams only order the same kernels); the caller's
-// pipe collides with exactly one of the four candidates, so exactly one choice is free of the
-// collision.  Lookup-only entry points open no side queue at all.
+// Round 6 (profiles/r06/queue_layout/): a program that opens one or two
+// streams (or one stream and a graph capture) BEFORE its first library call still gets a side
+// queue on its pipe.  Measured and not kept: reading the pipe from HW_REG_HW_ID (its pipe /
+// queue fields name the XCC-local dispatch path and are the same for every stream:
+// tools/microbench/hwid_probe.hip), and four candidate side streams with the one to leave out
+// learned per caller stream from timed calls (the learned choice was right in a clean process
+// but every choice timed slow in the first-streams layouts, though the same choice fixed from
+// the start ran at full speed: the cost depends on the queues' history, not only on their
+// order).  Kept: the side streams at the least priority (below), which leaves the caller's
+// normal-priority queues to the caller and makes a shared pipe cost +20% instead of +30%.
 struct SideStreams {
-    static constexpr int kC = 4;      // candidate side streams, opened back to back
-    static constexpr int kRoles = 3;  // early chains, regular chains, early hot columns
-    static constexpr int kEc = 0, kReg = 1, kEh = 2;
-    static constexpr int kPicks = 8;  // caller streams remembered per device
-    struct SidePick {
-        hipStream_t caller = nullptr;
-        uint64_t used = 0;             // LRU stamp (0: free)
-        int best = -1;                 // the candidate left out, once learned
-        int calls = 0;                 // full calls seen
-        uint32_t pending = 0;          // bit i: choice i's timing events are in flight
-        uint32_t timed = 0;            // bit i: choice i has a time
-        float ms[kC] = {0.f, 0.f, 0.f, 0.f};
-        hipEvent_t t0[kC] = {nullptr, nullptr, nullptr, nullptr};
-        hipEvent_t t1[kC] = {nullptr, nullptr, nullptr, nullptr};
-    };
+    static constexpr int kN = 4;  // early chains, regular chains, early hot columns, work
+    static constexpr int kEc = 0, kReg = 1, kEh = 2, kWork = 3;
     std::mutex mu;
-    hipStream_t st[kC] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t fork[kC] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t join[kC] = {nullptr, nullptr, nullptr, nullptr};
+    hipStream_t st[kN] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t fork[kN] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t join[kN] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t cand = nullptr;  // the hot-column candidates are picked (k_eh_pick)
-    SidePick picks[kPicks];
-    uint64_t stamp = 0;
 };
+
+// The work stream (kWork) exists only for the ET_WORK_STREAM experiment.
+inline int side_stream_count() { return ET_KNOB("ET_WORK_STREAM", 0) ? 4 : 3; }
 
 inline SideStreams* side_streams() {
     static SideStreams streams[64];
@@ -3138,137 +3136,56 @@ inline SideStreams* side_streams() {
     if (!ss.cand) {
         int least = 0, greatest = 0;
         if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
-        // ET_SIDE_PRIO=1 (experiment builds): the side streams at the least priority
-        const int prio = ET_KNOB("ET_SIDE_PRIO", 0) ? least : greatest;
-        for (int i = 0; i < SideStreams::kC; ++i)
+        const int n = side_stream_count();
+        // The side streams take the LEAST priority (round 6): their queues then come from the
+        // low-priority pool, not from the caller's normal-priority queues, and when one does
+        // share the caller's pipe the pipe favours the caller's dispatches — config 4 with
+        // one or two streams opened before the library's first call: 4.37-4.46 ms instead of
+        // 4.72-4.81 at the greatest priority; 3.66-3.71 ms in every other layout measured
+        // (profiles/r06/queue_layout/).  ET_SIDE_HIGH=1 (experiment builds): the greatest.
+        const int prio = ET_KNOB("ET_SIDE_HIGH", 0) ? greatest : least;
+        for (int i = 0; i < n; ++i)
             if ((!ss.fork[i] && hipEventCreateWithFlags(&ss.fork[i], hipEventDisableTiming)) ||
                 (!ss.join[i] && hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming)) ||
                 (!ss.st[i] &&
                  hipStreamCreateWithPriority(&ss.st[i], hipStreamNonBlocking, prio)))
                 return nullptr;
-        // acquire the four hardware queues now, back to back (an event record is a packet on
-        // the stream's queue), so they take four consecutive queue slots: one per pipe
-        for (int i = 0; i < SideStreams::kC; ++i)
+        // acquire the hardware queues now, back to back (an event record is a packet on the
+        // stream's queue)
+        for (int i = 0; i < n; ++i)
             if (hipEventRecord(ss.join[i], ss.st[i]) != hipSuccess) return nullptr;
         if (hipEventCreateWithFlags(&ss.cand, hipEventDisableTiming) != hipSuccess) return nullptr;
     }
     return &ss;
 }
 
-// The roles' candidates when candidate `skip` is left out.
-inline void side_roles(int skip, int (&c)[SideStreams::kRoles]) {
-    int k = 0;
-    for (int i = 0; i < SideStreams::kC && k < SideStreams::kRoles; ++i)
-        if (i != skip) c[k++] = i;
-}
-
-// fork(role, from): the role's side stream waits for everything `from` (default: the caller's
-// stream) has queued so far; the destructor joins every forked side stream into the caller's
-// stream (every return path of et_sparse_sgd), then closes a timed call (SidePick).
+// fork(i, from): side stream i waits for everything `from` (default: the caller's stream)
+// has queued so far; the destructor joins every forked side stream into the caller's stream
+// (every return path of et_sparse_sgd).
 struct SideFork {
     SideStreams* ss = nullptr;
     hipStream_t main = nullptr;
     std::unique_lock<std::mutex> lk;
-    int c[SideStreams::kRoles] = {0, 1, 2};
-    bool forked[SideStreams::kRoles] = {false, false, false};
-    SideStreams::SidePick* pick = nullptr;
-    int timing = -1;  // the choice this call times (its t1 is recorded at the call's end)
-    SideFork(SideStreams* s, hipStream_t m, bool full_call) : ss(s), main(m) {
-        if (!ss) return;
-        lk = std::unique_lock<std::mutex>(ss->mu);
-        choose(full_call);
+    bool forked[SideStreams::kN] = {false, false, false, false};
+    SideFork(SideStreams* s, hipStream_t m) : ss(s), main(m) {
+        if (ss) lk = std::unique_lock<std::mutex>(ss->mu);
     }
-    // The candidate to leave out for this caller stream: learned (see SideStreams), or the
-    // experiment knob ET_SIDE_SKIP.  While learning, full calls (not INDEX_ONLY / APPLY_ONLY,
-    // not capturing) after the first each time one choice not yet timed (events of their own,
-    // so no call waits for another's), and every call harvests the finished timings; the
-    // other calls leave out the last candidate.
-    void choose(bool full_call) {
-        constexpr int kC = SideStreams::kC;
-        const int forced = (int)ET_KNOB("ET_SIDE_SKIP", -1);
-        if (forced >= 0 && forced < kC) {
-            side_roles(forced, c);
-            return;
-        }
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        const bool capturing =
-            hipStreamIsCapturing(main, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
-        SideStreams::SidePick* p = nullptr;
-        for (auto& q : ss->picks)
-            if (q.used && q.caller == main) p = &q;
-        if (!p) {
-            if (capturing) {  // nothing learned for this stream: the last candidate out
-                side_roles(kC - 1, c);
-                return;
-            }
-            p = &ss->picks[0];
-            for (auto& q : ss->picks)
-                if (q.used < p->used) p = &q;  // a free slot, else the least recently used
-            SideStreams::SidePick fresh;
-            for (int i = 0; i < kC; ++i) {  // keep the slot's events
-                fresh.t0[i] = p->t0[i];
-                fresh.t1[i] = p->t1[i];
-            }
-            *p = fresh;
-            p->caller = main;
-            for (int i = 0; i < kC && p->best < 0; ++i)
-                if ((!p->t0[i] && hipEventCreate(&p->t0[i]) != hipSuccess) ||
-                    (!p->t1[i] && hipEventCreate(&p->t1[i]) != hipSuccess))
-                    p->best = kC - 1;  // no timing: keep the default
-        }
-        p->used = ++ss->stamp;
-        int skip = p->best;
-        if (skip < 0) {
-            for (int i = 0; i < kC; ++i)  // harvest the finished timings
-                if (((p->pending >> i) & 1u) && hipEventQuery(p->t1[i]) == hipSuccess) {
-                    float ms = 0.f;
-                    if (hipEventElapsedTime(&ms, p->t0[i], p->t1[i]) == hipSuccess) {
-                        p->ms[i] = ms;
-                        p->timed |= 1u << i;
-                    }
-                    p->pending &= ~(1u << i);
-                }
-            int next = -1, fastest = -1;
-            for (int i = 0; i < kC; ++i) {
-                if (!(((p->timed | p->pending) >> i) & 1u) && next < 0) next = i;
-                if (((p->timed >> i) & 1u) && (fastest < 0 || p->ms[i] < p->ms[fastest]))
-                    fastest = i;
-            }
-            if (p->timed == (1u << kC) - 1u) {
-                p->best = skip = fastest;  // every choice timed once: keep the fastest
-            } else if (next >= 0 && full_call && !capturing && p->calls > 0 &&
-                       hipEventRecord(p->t0[next], main) == hipSuccess) {
-                skip = next;  // time this choice on this call
-                p->pending |= 1u << next;
-                timing = next;
-            } else {
-                skip = kC - 1;
-            }
-        }
-        if (full_call && !capturing) ++p->calls;
-        pick = p;
-        side_roles(skip, c);
-    }
-    hipStream_t fork(int role, hipStream_t from = nullptr) {
+    hipStream_t fork(int i, hipStream_t from = nullptr) {
         if (!ss) return nullptr;
-        const int i = c[role];
-        if (!forked[role]) {
+        if (!forked[i]) {
             if (hipEventRecord(ss->fork[i], from ? from : main) != hipSuccess ||
                 hipStreamWaitEvent(ss->st[i], ss->fork[i], 0) != hipSuccess)
                 return nullptr;
-            forked[role] = true;
+            forked[i] = true;
         }
         return ss->st[i];
     }
     ~SideFork() {
-        if (!ss) return;
-        for (int r = 0; r < SideStreams::kRoles; ++r)
-            if (forked[r]) {
-                (void)hipEventRecord(ss->join[c[r]], ss->st[c[r]]);
-                (void)hipStreamWaitEvent(main, ss->join[c[r]], 0);
+        for (int i = 0; i < SideStreams::kN; ++i)
+            if (forked[i]) {
+                (void)hipEventRecord(ss->join[i], ss->st[i]);
+                (void)hipStreamWaitEvent(main, ss->join[i], 0);
             }
-        if (timing >= 0 && hipEventRecord(pick->t1[timing], main) != hipSuccess)
-            pick->pending &= ~(1u << timing);
     }
 };
 
@@ -3344,6 +3261,7 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
 extern "C" int et_sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, double eta,
                              uint32_t flags, void* workspace, int64_t ws_bytes, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     return sparse_sgd(dtype, descs, ntables, eta, flags, nullptr, workspace, ws_bytes, stream);
 }
 
@@ -3351,6 +3269,7 @@ extern "C" int et_sparse_sgd_snap(int dtype, const et_update_desc* descs, int32_
                                   double eta, uint32_t flags, int64_t* const* snaps,
                                   void* workspace, int64_t ws_bytes, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (!snaps) return et::fail(ET_ERR_ARG, "snaps is NULL");
     if (ntables > ET_MAX_TABLES_PER_LAUNCH)
         return et::fail(ET_ERR_ARG, "et_sparse_sgd_snap: at most %d tables per call",
@@ -3459,7 +3378,12 @@ static int sparse_sgd(int dtype, const et_update_desc* descs, int32_t ntables, d
     const et::EhMap ehm = et::eh_map(use_eh ? eh : et::EcList{});
     et::SideStreams* sides = chain ? et::side_streams() : nullptr;
     if (chain && !sides) return et::fail(ET_ERR_HIP, "sparse SGD: side streams unavailable");
-    et::SideFork fork(sides, s, !index_only && !apply_only);
+    et::SideFork fork(sides, s);
+    // ET_WORK_STREAM=1 (experiment builds): the main-line work on a library stream
+    if (chain && ET_KNOB("ET_WORK_STREAM", 0)) {
+        s = fork.fork(et::SideStreams::kWork);
+        if (!s) return et::fail(ET_ERR_HIP, "sparse SGD: side stream fork failed");
+    }
     hipStream_t ec_side = nullptr;
     if (use_ec) {
         ec_side = fork.fork(et::SideStreams::kEc);
@@ -3650,6 +3574,7 @@ extern "C" int et_index_build(const int64_t* idx, int32_t pool, int64_t ld_idx, 
                               int64_t* map, int64_t* nunique_dev, void* workspace,
                               int64_t ws_bytes, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (pool < 0 || batch < 0 || nrows < 0) return et::fail(ET_ERR_ARG, "negative size");
     const int64_t n = (int64_t)pool * batch;
     if (n >= 0x7fffffffll) return et::fail(ET_ERR_ARG, "too many occurrences");
@@ -3776,6 +3701,7 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
                                  int64_t ubegin, int64_t uend, const int64_t* map, double eta,
                                  uint32_t flags, void* stream) {
     et::clear_err();
+    et::open_side_streams(static_cast<hipStream_t>(stream));
     if (dtype != ET_F32 && dtype != ET_F64 && dtype != ET_F16 && dtype != ET_BF16)
         return et::fail(ET_ERR_UNSUPPORTED, "update: dtype %d", dtype);
     if (uend <= ubegin || dim == 0) return ET_OK;
@@ -3804,6 +3730,19 @@ extern "C" int et_update_indexed(int dtype, void* table, int64_t ld_table,
 
 ET_OOB_READER(update)
 
+namespace et {
+// Open this device's side queues at the first library call (see SideStreams); a no-op after
+// that, and while the caller's stream is capturing a graph.
+void open_side_streams(hipStream_t caller) {
+    static std::atomic<uint64_t> done{0};  // bit d: device d's side streams are open
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+    if (done.load(std::memory_order_relaxed) & (1ull << dev)) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(caller, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    if (side_streams()) done.fetch_or(1ull << dev);
+}
+}  // namespace et
 
 #ifdef ET_EXPERIMENTS
 // Experiment builds only: copy (and reset) the chain-item timeline, 2 x uint4 per item
