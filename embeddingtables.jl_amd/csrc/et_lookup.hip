@@ -843,6 +843,83 @@ __global__ __launch_bounds__(256) void k_gather_vec(LookupPack pack, int ntables
     }
 }
 
+// Non-reducing gather (config 2, round 6): one round per workgroup of W waves, each lane group
+// (RB / 16 lanes, one 16-byte vector each) holding its U rows in flight at once and storing each
+// as it arrives (vector loads return in order, so the store of row u waits for rows 0..u only).
+// U = 8, W = 4 — 1,024 workgroups at B = 65,536 — measured 14.32-14.40 us per graph-replayed
+// launch against 15.25 for round 5's k_gather_pipe (two rounds of 8 in 512 workgroups), U = 16
+// 15.6-15.8, U = 4 / W = 8 14.9, U = 6 / 12 15.6-15.9, W = 2 / 8 / 1 14.48-14.58 / 14.40-14.43 /
+// 14.87 (profiles/r06/cfg2_variants.txt; ET_GATHER_ONE / ET_GATHER_W in experiment builds).
+template <int RB, bool NT, bool NTL, int U, int W = 4>
+__global__ __launch_bounds__(64 * W) void k_gather_one(LookupPack pack, int ntables, int64_t batch,
+                                                       char* __restrict__ dst, int64_t ld_dst_b,
+                                                       int es) {
+#ifdef ET_WG_TIMELINE
+    const uint64_t tl0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    constexpr int VPR = RB / 16;
+    static_assert(VPR <= 64 && 64 % VPR == 0, "one vector per lane");
+    constexpr int GPW = 64 / VPR;
+    const int64_t item = blockIdx.x;
+    const int t = (int)(item % ntables);
+    const int64_t chunk = item / ntables;
+    const et_lookup_desc& d = pack.d[t];
+    const char* table = reinterpret_cast<const char*>(d.table);
+    const int64_t ld_b = d.ld_table * es;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane / VPR, sub = lane % VPR;
+    const int64_t per_round = W * GPW;
+    const int64_t bag0 = chunk * per_round * U + wave * GPW + g;
+    int64_t iv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        int64_t b = bag0 + u * per_round;
+        b = b < batch ? b : batch - 1;
+        iv[u] = d.idx[b * d.ld_idx];
+    }
+    u32x4 cur[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t row = (uint64_t)(iv[u] - 1);
+        ok[u] = row < (uint64_t)d.nrows;
+        const u32x4* src = reinterpret_cast<const u32x4*>(table + (ok[u] ? row * (uint64_t)ld_b : 0)) + sub;
+        if constexpr (NTL) cur[u] = __builtin_nontemporal_load(src);
+        else cur[u] = *src;
+    }
+#ifdef ET_WG_TIMELINE
+    asm volatile("" ::: "memory");
+    const uint64_t tl1 = __builtin_amdgcn_s_memrealtime();  // indices in, rows issued
+#endif
+    int bad = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t bag = bag0 + u * per_round;
+        if (bag < batch) {
+            bad += ok[u] ? 0 : 1;
+            u32x4* o = reinterpret_cast<u32x4*>(dst + bag * ld_dst_b + d.dst_row_off * es) + sub;
+            store16<NT>(o, ok[u] ? cur[u] : u32x4{0u, 0u, 0u, 0u});
+        }
+    }
+    if (bad && sub == 0) note_oob(bad);
+#ifdef ET_WG_TIMELINE
+    // Profiling build only (tools/gather_timeline.py): wave 0's start, the moment its row
+    // loads are issued (its indices have arrived), and the workgroup's end with every store
+    // complete, on the 100 MHz constant clock
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < kTlCap) {
+        const uint64_t tl2 = __builtin_amdgcn_s_memrealtime();
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_tl[blockIdx.x][0] = make_uint4((uint32_t)tl0, (uint32_t)(tl0 >> 32), (uint32_t)tl1,
+                                         (uint32_t)(tl1 >> 32));
+        g_tl[blockIdx.x][1] = make_uint4((uint32_t)tl2, (uint32_t)(tl2 >> 32), xcc, gridDim.x);
+    }
+#endif
+}
+
+#ifdef ET_EXPERIMENTS
 // The same gather, software-pipelined over `rounds` rounds per workgroup: round r + 1's rows
 // are loaded before round r's are stored, and round r + 2's indices before those, so each
 // wave keeps a round of rows in flight while it writes the previous one.  The one-round
@@ -928,6 +1005,8 @@ __global__ __launch_bounds__(256) void k_gather_pipe(LookupPack pack, int ntable
     }
     if (bad && sub == 0) note_oob(bad);
 }
+#endif  // ET_EXPERIMENTS: round 5's two-round gather (ET_GATHER_PIPE=2..)
+
 
 // Generic path: any feature size / alignment / per-table dims / paged tables.  One wave
 // per bag, lanes stride over the features, pool order sequential per feature.
@@ -1255,10 +1334,6 @@ int launch_pooled_vec_u(const LookupPack& pack, int n, int64_t batch, void* dst,
     return ET_OK;
 }
 
-// Config 2, graph-replayed (tools/cfg2_trace.py, one box, twice): 1 round (k_gather_vec)
-// 19.21 us per launch, 2 rounds 16.00-16.02, 4 rounds 17.00-17.04 (profiles/r05/cfg2/).
-constexpr int kGatherPipeRounds = 2;
-
 template <int RB, bool NT>
 int launch_gather_rb(const LookupPack& pack, int n, int64_t batch, void* dst, int64_t ld_dst,
                      int es, hipStream_t s) {
@@ -1268,28 +1343,69 @@ int launch_gather_rb(const LookupPack& pack, int n, int64_t batch, void* dst, in
     constexpr int U = NV >= 8 ? 1 : 8 / NV;
     const int64_t per_round = 4 * (64 / LPR) * U;
     if constexpr (NV == 1 && U == 8) {
-        // pipelined over kGatherPipeRounds rounds (k_gather_pipe) when the launch still has
-        // at least 256 workgroups; ET_GATHER_PIPE (experiment builds) sets the rounds, 1 = off
-        const int pr = (int)ET_KNOB("ET_GATHER_PIPE", kGatherPipeRounds);
-        const int64_t g = (batch + per_round * pr - 1) / (per_round * pr) * n;
-        if (pr > 1 && g >= 256) {
+        // rows of tables larger than the Infinity Cache load non-temporally, as the pooled
+        // kernels' (ntload_bytes): config 2 15.26-15.29 vs 15.99-16.04 us per launch in round 5
+        // (profiles/r05/cfg2/ab_gather_pipe.txt)
+        bool ntl = tuning().ntload != 0;
+        for (int t = 0; t < n && ntl; ++t)
+            ntl = pack.d[t].nrows * pack.d[t].ld_table * es > tuning().ntload_bytes;
+        bool one = true;
+#ifdef ET_EXPERIMENTS
+        // ET_GATHER_PIPE=R (R >= 2): round 5's k_gather_pipe over R rounds; 1: k_gather_vec
+        const int pr = (int)ET_KNOB("ET_GATHER_PIPE", 0);
+        one = pr == 0;
+        const int64_t g = pr > 1 ? (batch + per_round * pr - 1) / (per_round * pr) * n : 0;
+        if (pr > 1 && g >= 1) {
             if (g > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
-            // rows of tables larger than the Infinity Cache load non-temporally, as the pooled
-            // kernels' (ntload_bytes): config 2 15.26-15.29 vs 15.99-16.04 us per launch
-            // (profiles/r05/cfg2/ab_gather_pipe.txt)
-            bool ntl = tuning().ntload != 0;
-            for (int t = 0; t < n && ntl; ++t)
-                ntl = pack.d[t].nrows * pack.d[t].ld_table * es > tuning().ntload_bytes;
-            if (ntl) {
+            if (ntl)
                 hipLaunchKernelGGL((k_gather_pipe<RB, NT, true>), dim3((unsigned)g), dim3(256), 0,
                                    s, pack, n, batch, reinterpret_cast<char*>(dst), ld_dst * es,
                                    es, pr);
-                ET_LAUNCH_CHECK("k_gather_pipe");
-                return ET_OK;
-            }
-            hipLaunchKernelGGL((k_gather_pipe<RB, NT>), dim3((unsigned)g), dim3(256), 0, s, pack,
-                               n, batch, reinterpret_cast<char*>(dst), ld_dst * es, es, pr);
+            else
+                hipLaunchKernelGGL((k_gather_pipe<RB, NT>), dim3((unsigned)g), dim3(256), 0, s,
+                                   pack, n, batch, reinterpret_cast<char*>(dst), ld_dst * es, es,
+                                   pr);
             ET_LAUNCH_CHECK("k_gather_pipe");
+            return ET_OK;
+        }
+        if (const int uo = (int)ET_KNOB("ET_GATHER_ONE", 0)) {  // U / W variants of k_gather_one
+            const int w = (int)ET_KNOB("ET_GATHER_W", 4);
+            const int64_t pw = w * (64 / LPR) * uo;
+            const int64_t g1 = (batch + pw - 1) / pw * n;
+            if (g1 > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+#define ET_G1(UU, WW)                                                                            \
+    if (uo == UU && w == WW) {                                                                   \
+        if (ntl)                                                                                 \
+            hipLaunchKernelGGL((k_gather_one<RB, NT, true, UU, WW>), dim3((unsigned)g1),        \
+                               dim3(64 * WW), 0, s, pack, n, batch,                              \
+                               reinterpret_cast<char*>(dst), ld_dst * es, es);                   \
+        else                                                                                     \
+            hipLaunchKernelGGL((k_gather_one<RB, NT, false, UU, WW>), dim3((unsigned)g1),       \
+                               dim3(64 * WW), 0, s, pack, n, batch,                              \
+                               reinterpret_cast<char*>(dst), ld_dst * es, es);                   \
+        ET_LAUNCH_CHECK("k_gather_one");                                                         \
+        return ET_OK;                                                                            \
+    }
+            ET_G1(4, 4) ET_G1(16, 4) ET_G1(32, 4) ET_G1(6, 4) ET_G1(12, 4)
+            ET_G1(8, 2) ET_G1(8, 8) ET_G1(8, 1) ET_G1(16, 2) ET_G1(4, 8)
+#undef ET_G1
+        }
+#endif
+        if (one) {  // the default: one round of 8 rows per lane group, 4 waves per workgroup
+            constexpr int kU = 8, kW = 4;
+            const int64_t pw = kW * (64 / LPR) * kU;
+            const int64_t g1 = (batch + pw - 1) / pw * n;
+            if (g1 <= 0) return ET_OK;
+            if (g1 > 0x7fffffffll) return fail(ET_ERR_ARG, "grid too large");
+            if (ntl)
+                hipLaunchKernelGGL((k_gather_one<RB, NT, true, kU, kW>), dim3((unsigned)g1),
+                                   dim3(64 * kW), 0, s, pack, n, batch,
+                                   reinterpret_cast<char*>(dst), ld_dst * es, es);
+            else
+                hipLaunchKernelGGL((k_gather_one<RB, NT, false, kU, kW>), dim3((unsigned)g1),
+                                   dim3(64 * kW), 0, s, pack, n, batch,
+                                   reinterpret_cast<char*>(dst), ld_dst * es, es);
+            ET_LAUNCH_CHECK("k_gather_one");
             return ET_OK;
         }
     }

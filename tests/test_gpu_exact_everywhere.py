@@ -212,3 +212,71 @@ def test_queue_blocks_per_thread_and_stream(oracle):
     assert not errs, errs
     assert not any(t.is_alive() for t in th)
     assert not bad
+
+
+@pytest.mark.parametrize("kind", ["f64", "f16", "f16acc", "bf16"])
+def test_default_exact_typed_early_hot_columns(oracle, kind):
+    """the typed chain walk on the EARLY HOT list (k_sgd_chains_x<T, C> and the EH
+    plan on non-Float32 tables).  A 3,000-row table at B = 65,536, pool 20: its hottest Zipf
+    columns (~140 K occurrences, above the 32,768 the sampled plan needs) are early hot
+    columns, the next ones regular chains; single-table default update!, every column
+    bit-identical to the oracle's typed model."""
+    from oracle import f32_to_bf16
+
+    from embtab.tables import fused_update_path
+
+    rng = np.random.default_rng(31)
+    Bb, P, dim, R = 65536, 20, 64, 3000
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(32)
+    npdt = {"f64": np.float64, "f16": np.float16, "f16acc": np.float16}
+    x = rng.standard_normal((R, dim)).astype(np.float32)
+    d = rng.standard_normal((Bb, dim)).astype(np.float32)
+    if kind == "bf16":
+        base, delta = f32_to_bf16(x), f32_to_bf16(d)
+    else:
+        base, delta = x.astype(npdt[kind]), d.astype(npdt[kind])
+    I = _zipf(R, (Bb, P), gen)
+    tdev, ddev = torch.from_numpy(base).to(DEV), torch.from_numpy(delta).to(DEV)
+    if kind == "bf16":
+        tdev, ddev = tdev.view(torch.bfloat16), ddev.view(torch.bfloat16)
+    A = et.SimpleEmbedding(tdev, et.Static(dim))
+    et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, ddev, I),
+               f16_fp32_acc=kind == "f16acc")
+    ref = base.copy()
+    oracle.sgd(ref, delta, I.cpu().numpy(), 0.1, fused=fused_update_path(A), bf16=kind == "bf16",
+               f16_fp32_acc=kind == "f16acc")
+    counts = np.bincount(I.cpu().numpy().ravel(), minlength=R + 1)[1:]
+    assert counts.max() > 2 * 32768  # early hot columns
+    got = (A.data.view(torch.int16) if kind != "f64" else A.data).cpu().numpy()
+    assert got.tobytes() == ref.view(got.dtype).tobytes(), kind
+    assert et.check_errors() == 0
+
+
+def test_default_exact_f32_wide_walk_for_a_long_gradient_stride(oracle):
+    """the Float32 chain walk with 64-bit addresses when the gradient's stride
+    reaches 2^22 elements (chain_asm_ok fails on ld, not on the batch): a 3-row table's early
+    chains (hottest column ~700 occurrences) at B = 64, pool 20, with the gradient a column
+    block of a (64, 2^22 + 256) matrix, bit-identical to the oracle."""
+    Bb, P, dim, R = 64, 20, 128, 3
+    ld = (1 << 22) + 256
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(41)
+    big = torch.empty((Bb, ld), dtype=torch.float32, device=DEV)  # 1.07 GB
+    L = _lib.load()
+    _lib.check(L.et_fill_uniform(_lib.ET_F32, big.data_ptr(), big.numel(), 4100, 0, -1.0, 1.0,
+                                 _lib.stream_handle()))
+    delta = big[:, ld - dim:]
+    assert delta.stride(0) >= (1 << 22)
+    x = torch.rand((R, dim), generator=gen, device=DEV, dtype=torch.float32)
+    I = _zipf(R, (Bb, P), gen)
+    A = et.SimpleEmbedding(x.clone(), et.Static(dim))
+    et.update_(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, delta, I))
+    ref = x.cpu().numpy()
+    oracle.sgd(ref, delta.cpu().numpy(), I.cpu().numpy(), 0.1, fused=True)
+    counts = np.bincount(I.cpu().numpy().ravel(), minlength=R + 1)[1:]
+    assert counts.max() > 256  # a chain
+    assert A.data.cpu().numpy().tobytes() == ref.tobytes()
+    assert et.check_errors() == 0
+    del big
+    torch.cuda.empty_cache()

@@ -1,9 +1,8 @@
-"""The pipelined vector-index gather (k_gather_pipe, et_lookup.hip): launches of at least 256
-workgroups of two rounds each — batches from 32,768 bags of 512-byte rows — load round r + 1's
-rows before storing round r's.  Bit copies of the oracle's gather (src/lookup.jl:51-87) at
-every row size the kernel takes (128 .. 1024 bytes), batches that end inside a workgroup, a
-row group and a round, a strided destination, several tables in one launch and out-of-range
-indices (zero rows, counted)."""
+"""The vector-index gather (k_gather_one, et_lookup.hip; round 5's pipelined k_gather_pipe
+before it): one round of 8 rows per lane group, each row stored as it arrives.  Bit copies of
+the oracle's gather (src/lookup.jl:51-87) at every row size the kernel takes (128 .. 1024
+bytes), batches that end inside a workgroup and a row group, a strided destination, several
+tables in one launch and out-of-range indices (zero rows, counted)."""
 import numpy as np
 import pytest
 import torch

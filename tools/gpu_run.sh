@@ -183,6 +183,14 @@ print('$SETS $c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric'
         python3 tools/queue_map.py "$f" > "$OUT/qmap_$m.txt" && rm -rf "$OUT/qmap_$m"
         echo "$m $(tail -1 "$OUT/qmap_$m.json")"
       done ;;
+    shardq)
+      # queue / stream map of the world-1 sharded step (lookups + exchange stream), ADVICE r05
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/shardq" -o run --output-format csv \
+        -- python3 bench.py --force-shard --steps 10 --warmup 2 --no-extra --cpu-seconds 0 \
+        > "$OUT/shardq.json" 2> "$OUT/shardq.err" || die shardq "$OUT/shardq.err"
+      f=$(ls "$OUT"/shardq/*/run_kernel_trace.csv "$OUT"/shardq/run_kernel_trace.csv 2>/dev/null | head -1)
+      python3 tools/queue_map.py "$f" > "$OUT/shardq.txt" && rm -rf "$OUT/shardq"
+      grep -E "queue" "$OUT/shardq.txt" | cut -c1-100 ;;
     expcapture:*)
       IFS=: read -r _ SETS MODES <<< "$step"
       for m in $(echo "$MODES" | tr ',' ' '); do
