@@ -920,6 +920,62 @@ __global__ __launch_bounds__(64 * W) void k_gather_one(LookupPack pack, int ntab
 }
 
 #ifdef ET_EXPERIMENTS
+// Experiment (ET_GATHER_S=1, config 2): 512-byte rows with the indices read through the SCALAR
+// cache — each wave's 16 contiguous bags' indices by scalar loads (vector indices, ld_idx = 1),
+// so the index reads do not queue behind the row reads in the CU's vector memory path (the
+// gather timeline shows wave 0's index loads returning after 1-8 us) — then k_gather_one's
+// round: 8 rows per half-wave in flight, each stored as it arrives.
+template <bool NT, bool NTL>
+__global__ __launch_bounds__(256) void k_gather_s512(LookupPack pack, int ntables, int64_t batch,
+                                                     char* __restrict__ dst, int64_t ld_dst_b,
+                                                     int es) {
+    const int64_t item = blockIdx.x;
+    const int t = (int)(item % ntables);
+    const int64_t chunk = item / ntables;
+    const et_lookup_desc& d = pack.d[t];
+    const char* table = reinterpret_cast<const char*>(d.table);
+    const uint64_t ld_b = (uint64_t)(d.ld_table * es);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int hi = lane >= 32 ? 1 : 0;
+    const int sub = lane & 31;
+    const int64_t base = chunk * 64 + wave * 16;
+    if (base >= batch) return;  // wave-uniform
+    const cidx_ptr ip = as_scalar_idx(d.idx + base);
+    int64_t iv[16];
+    if (base + 16 <= batch) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) iv[k] = ip[k];
+    } else {
+        const int64_t last = batch - 1 - base;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) iv[k] = ip[k < last ? k : last];
+    }
+    u32x4 cur[8];
+    bool ok[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const uint64_t row = (uint64_t)((hi ? iv[2 * u + 1] : iv[2 * u]) - 1);
+        ok[u] = row < (uint64_t)d.nrows;
+        const u32x4* src = reinterpret_cast<const u32x4*>(table + (ok[u] ? row * ld_b : 0)) + sub;
+        if constexpr (NTL) cur[u] = __builtin_nontemporal_load(src);
+        else cur[u] = *src;
+    }
+    int bad = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int64_t bag = base + 2 * u + hi;
+        if (bag < batch) {
+            bad += ok[u] ? 0 : 1;
+            u32x4* o = reinterpret_cast<u32x4*>(dst + bag * ld_dst_b + d.dst_row_off * es) + sub;
+            store16<NT>(o, ok[u] ? cur[u] : u32x4{0u, 0u, 0u, 0u});
+        }
+    }
+    if (bad && sub == 0) note_oob(bad);
+}
+#endif
+
+#ifdef ET_EXPERIMENTS
 // The same gather, software-pipelined over `rounds` rounds per workgroup: round r + 1's rows
 // are loaded before round r's are stored, and round r + 2's indices before those, so each
 // wave keeps a round of rows in flight while it writes the previous one.  The one-round
@@ -1367,6 +1423,23 @@ int launch_gather_rb(const LookupPack& pack, int n, int64_t batch, void* dst, in
                                    pr);
             ET_LAUNCH_CHECK("k_gather_pipe");
             return ET_OK;
+        }
+        if constexpr (RB == 512) {
+            bool contig = ET_KNOB("ET_GATHER_S", 0) != 0;
+            for (int t = 0; t < n && contig; ++t) contig = pack.d[t].ld_idx == 1;
+            if (contig) {
+                const int64_t gs = (batch + 63) / 64 * n;
+                if (ntl)
+                    hipLaunchKernelGGL((k_gather_s512<NT, true>), dim3((unsigned)gs), dim3(256), 0,
+                                       s, pack, n, batch, reinterpret_cast<char*>(dst),
+                                       ld_dst * es, es);
+                else
+                    hipLaunchKernelGGL((k_gather_s512<NT, false>), dim3((unsigned)gs), dim3(256),
+                                       0, s, pack, n, batch, reinterpret_cast<char*>(dst),
+                                       ld_dst * es, es);
+                ET_LAUNCH_CHECK("k_gather_s512");
+                return ET_OK;
+            }
         }
         if (const int uo = (int)ET_KNOB("ET_GATHER_ONE", 0)) {  // U / W variants of k_gather_one
             const int w = (int)ET_KNOB("ET_GATHER_W", 4);
