@@ -311,15 +311,24 @@ def _update_desc(table: AbstractEmbeddingTable, grad: SparseEmbeddingUpdate) -> 
                            I.data_ptr(), 1 if I.dim() == 1 else _ld(I), B, cpp)
 
 
-def _sparse_sgd(descs, eta: float, flags: int, device, dtype=torch.float32):
+def _sparse_sgd(descs, eta: float, flags: int, device, dtype=torch.float32, snaps=None):
+    """One et_sparse_sgd call; `snaps` (one device pointer or None per descriptor) makes it
+    et_sparse_sgd_snap, whose key pass copies those tables' index arrays."""
     L = _lib.load()
     n = len(descs)
     arr = (_lib.UpdateDesc * n)(*descs)
     nb = ctypes.c_int64(0)
     _lib.check(L.et_sgd_workspace_size(ctypes.addressof(arr), n, ctypes.byref(nb)))
     ws = _workspace(nb.value, device, "sgd")
-    _lib.check(L.et_sparse_sgd(_lib.TORCH_TO_ET[dtype], ctypes.addressof(arr), n, float(eta),
-                               flags, ws.data_ptr(), ws.numel(), _lib.stream_handle(device)))
+    stream = _lib.stream_handle(device)
+    if snaps is not None and any(snaps):
+        sarr = (ctypes.c_void_p * n)(*snaps)
+        _lib.check(L.et_sparse_sgd_snap(_lib.TORCH_TO_ET[dtype], ctypes.addressof(arr), n,
+                                        float(eta), flags, ctypes.addressof(sarr), ws.data_ptr(),
+                                        ws.numel(), stream))
+    else:
+        _lib.check(L.et_sparse_sgd(_lib.TORCH_TO_ET[dtype], ctypes.addressof(arr), n, float(eta),
+                                   flags, ws.data_ptr(), ws.numel(), stream))
 
 
 # The exact update (every column's gradient summed serially in the reference's order,
@@ -362,7 +371,8 @@ def update_(*args, nontemporal: bool | None = None, exact: bool | None = None,
         if isinstance(args[1], AbstractEmbeddingTable):
             table, grad = args[1], args[2]
             nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
-            _update_single(opt, table, grad, nt, exact, f16_fp32_acc, hot_pass)
+            indexer = args[3] if len(args) > 3 else kw.get("indexer")
+            _update_single(opt, table, grad, nt, exact, f16_fp32_acc, hot_pass, indexer)
             return None
         tables, grads = list(args[1]), list(args[2])
         nt = args[4] if len(args) > 4 else (True if nontemporal is None else nontemporal)
@@ -377,15 +387,25 @@ def update_(*args, nontemporal: bool | None = None, exact: bool | None = None,
 
 
 def _update_single(opt: Descent, table, grad: SparseEmbeddingUpdate, nontemporal: bool,
-                   exact: bool, f16_fp32_acc: bool = False, hot_pass: bool = False):
+                   exact: bool, f16_fp32_acc: bool = False, hot_pass: bool = False,
+                   indexer=None):
+    """src/sparseupdate.jl:159-178: ``index!(indexer, update.indices, size(table, 2))``, then
+    the update from it.  The device pipeline indexes on its own; a caller-supplied Indexer is
+    filled as the reference's is, from a snapshot of the indices the update's key pass takes
+    (et_sparse_sgd_snap), built into the reference layout on first use (Indexer._defer)."""
     if grad.indices.numel() == 0:
+        if isinstance(indexer, Indexer):
+            indexer._pending = (grad.indices, int(table.size()[1]))
         return
     d = _update_desc(table, grad)
     fused = fused_update_path(table)
+    snap = None
+    if isinstance(indexer, Indexer):
+        snap = indexer._defer(grad.indices, table.size()[1])
     # convert(eltype(table), opt.eta): the library rounds eta to the table type itself
     _sparse_sgd([d], opt.eta, _sgd_flags(fused, nontemporal, False, exact, f16_fp32_acc,
                                          hot_pass),
-                table.device, table.dtype)
+                table.device, table.dtype, [snap.data_ptr() if snap is not None else None])
 
 
 def _update_multi(opt: Descent, tables, grads, nontemporal: bool, exact: bool | None,

@@ -349,14 +349,24 @@ function _workspace(nbytes)
     return ws
 end
 
-function _sparse_sgd(::Type{T}, descs::Vector{UpdateDesc}, eta::Float64, flags::UInt32) where {T}
+# One update call; snapshot pointers (C_NULL for none) make it et_sparse_sgd_snap.
+function _sparse_sgd(::Type{T}, descs::Vector{UpdateDesc}, eta::Float64, flags::UInt32,
+                     snaps::Vector{Ptr{Int64}} = Ptr{Int64}[]) where {T}
     nb = Ref{Int64}(0)
     check(ccall((:et_sgd_workspace_size, libembtab), Cint, (Ptr{UpdateDesc}, Int32, Ref{Int64}),
                 descs, length(descs), nb))
     ws = _workspace(nb[])
-    check(ccall((:et_sparse_sgd, libembtab), Cint,
-                (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
-                et_dtype(T), descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
+    if any(p -> p != C_NULL, snaps)
+        check(ccall((:et_sparse_sgd_snap, libembtab), Cint,
+                    (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Ptr{Int64}}, Ptr{Cvoid},
+                     Int64, Ptr{Cvoid}),
+                    et_dtype(T), descs, length(descs), eta, flags, snaps, ws.ptr, length(ws),
+                    stream()))
+    else
+        check(ccall((:et_sparse_sgd, libembtab), Cint,
+                    (Cint, Ptr{UpdateDesc}, Int32, Float64, UInt32, Ptr{Cvoid}, Int64, Ptr{Cvoid}),
+                    et_dtype(T), descs, length(descs), eta, flags, ws.ptr, length(ws), stream()))
+    end
 end
 
 # The exact update (every column's gradient summed serially in the reference's order) is
@@ -368,14 +378,24 @@ const EXACT = Ref{Union{Nothing,Bool}}(nothing)
 _exact_flag(exact) = exact === nothing ? ET_FLAG_EXACT_IF_FAST :
                      exact ? ET_FLAG_EXACT_UPDATE : UInt32(0)
 
+# src/sparseupdate.jl:159-178 indexes into `indexer` first (index!(indexer, update.indices,
+# size(table, 2))): a HipIndexer receives a snapshot of the indices from the update's own key
+# pass (et_sparse_sgd_snap, built when first read), a host Indexer passed by the caller the
+# reference's own index! on a downloaded copy; with none (the default here, where the
+# reference's default is a fresh Indexer() nobody can read) nothing is indexed.
 function update!(opt::Flux.Descent, table::HipTable{S,T}, grad::SparseEmbeddingUpdate,
-                 indexer = Indexer(), ::Val{Nontemporal} = Val(true),
+                 indexer = nothing, ::Val{Nontemporal} = Val(true),
                  args...; exact::Union{Nothing,Bool} = EXACT[]) where {S,T<:UpdateEltype,Nontemporal}
     flags = (Nontemporal ? ET_FLAG_NONTEMPORAL : UInt32(0)) |
             (_fused(table) ? UInt32(0) : ET_FLAG_SGD_UNFUSED) |
             _exact_flag(exact)
+    snap = indexer isa HipIndexer && !isempty(grad.indices) ?
+           _snapshot!(indexer, grad.indices, size(table, 2)) : Ptr{Int64}(C_NULL)
     # convert(eltype(table), opt.eta) happens inside the library
-    _sparse_sgd(T, [_update_desc(table, grad)], Float64(opt.eta), flags)
+    _sparse_sgd(T, [_update_desc(table, grad)], Float64(opt.eta), flags, Ptr{Int64}[snap])
+    if indexer isa AbstractIndexer && !(indexer isa HipIndexer)
+        EmbeddingTables.index!(indexer, download(grad.indices), size(table, 2))
+    end
     return nothing
 end
 

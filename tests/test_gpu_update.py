@@ -619,6 +619,35 @@ def test_indexers_snapshot_the_indices_of_their_update(oracle):
         assert np.array_equal(host(indexers[t].map), mp)
 
 
+def test_single_table_update_fills_its_indexer(oracle):
+    """The single-table update!(opt, table, grad, indexer) indexes into `indexer` first
+    (src/sparseupdate.jl:159-178: index!(indexer, update.indices, size(table, 2))), so a
+    caller-supplied Indexer holds the reference's cumulative / map of THOSE indices after the
+    call — from the update's own snapshot, even if the index buffer is refilled before it is
+    read — and the table gets the oracle's update; Flux.Optimise.update! the same.  Vector
+    and matrix indices, a hot column (a chain in the default exact mode)."""
+    rng = np.random.default_rng(177)
+    for shape in ((512, 20), (3000,)):
+        R, D = 400, 64
+        h = rng.standard_normal((R, D)).astype(np.float32)
+        I = rng.integers(1, R + 1, shape)
+        if len(shape) == 2:
+            I[:, :3] = 7  # 1,536 occurrences of column 7
+        delta = rng.standard_normal((shape[0], D)).astype(np.float32)
+        for upd in (lambda *a: et.update_(*a), lambda o, A, g, ix: et.optimise_update_(o, A, g, ix)):
+            A = et.SimpleEmbedding(dev(h), et.Static(D))
+            Idev = dev(I)
+            ix = et.Indexer()
+            upd(et.Descent(0.1), A, et.SparseEmbeddingUpdate(A.lookup_type, dev(delta), Idev), ix)
+            Idev.copy_(torch.from_numpy(rng.integers(1, R + 1, shape)))  # refilled in place
+            cum, mp = oracle.index_build(I, R)
+            assert np.array_equal(host(ix.cumulative), cum)
+            assert np.array_equal(host(ix.map), mp)
+            w = h.copy()
+            oracle.sgd(w, delta, I, 0.1, fused=True)
+            assert bits_equal(host(A.data), w)
+
+
 def test_hot_pass_with_unaligned_preallocation_gradient(oracle):
     """hot_pass=True on a Preallocation gradient whose row blocks are not 16-byte aligned
     (prependrows k = 1): the host drops the hot-column pass for that group instead of

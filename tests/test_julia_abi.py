@@ -183,3 +183,18 @@ def test_multi_table_update_fills_host_indexers_by_default():
     assert body.rfind("if fill_host_indexers", 0, host) != -1
     # before the telemetry callback and the apply phase (the reference's phase order)
     assert host < body.index("telemetry_cb()") < body.index("apply_phase()", host)
+
+
+def test_single_table_update_fills_a_given_indexer():
+    """src/sparseupdate.jl:159-178 indexes into the caller's `indexer` before updating: the
+    shim's single-table update! snapshots for a HipIndexer (et_sparse_sgd_snap through
+    _sparse_sgd) and fills a host Indexer with the reference's index!."""
+    src = open(SHIM).read()
+    m = re.search(r"function update!\(opt::Flux\.Descent, table::HipTable\{S,T\}.*?^end", src,
+                  re.S | re.M)
+    assert m, "single-table update! not found"
+    body = m.group(0)
+    assert "_snapshot!(indexer, grad.indices" in body
+    assert "EmbeddingTables.index!(indexer, download(grad.indices)" in body
+    m = re.search(r"function _sparse_sgd\(.*?^end", src, re.S | re.M)
+    assert m and "ccall((:et_sparse_sgd_snap, libembtab)" in m.group(0)
