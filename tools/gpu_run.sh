@@ -183,6 +183,13 @@ print('$SETS $c', t['tables'], 'tables', round(t['ms_median'],4), 'ms', 'fabric'
         python3 tools/queue_map.py "$f" > "$OUT/qmap_$m.txt" && rm -rf "$OUT/qmap_$m"
         echo "$m $(tail -1 "$OUT/qmap_$m.json")"
       done ;;
+    benchargs:*)
+      # the headline launch (kernel ms) with extra bench.py arguments ('+'-separated), e.g.
+      # benchargs:--min-rows+313 (the tables above 312 rows only)
+      A=$(echo "${step#benchargs:}" | tr '+' ' ')
+      timeout -k 10 200 python3 bench.py --steps 40 --warmup 5 --cpu-seconds 0 --no-extra --no-check $A \
+        > "$OUT/benchargs.json" 2> "$OUT/benchargs.err" || die benchargs "$OUT/benchargs.err"
+      python3 -c "import json; d=json.load(open('$OUT/benchargs.json')); print('$A', d['config']['tables'], 'tables', round(d['roofline']['kernel_ms'],4), round(d['roofline']['kernel_ms_median'],4))" ;;
     shardq)
       # queue / stream map of the world-1 sharded step (lookups + exchange stream), ADVICE r05
       timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/shardq" -o run --output-format csv \
