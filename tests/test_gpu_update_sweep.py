@@ -1,0 +1,152 @@
+"""A seeded random sweep of the default (exact) update against the oracle: table storage
+(contiguous, paged with a random page size, device column pointers), element type (Float32,
+Float64, Float16 with Julia's Float16 arithmetic or Float32 sums, BFloat16), rows, dim, pool,
+batch and Zipf or uniform indices drawn at random per case — every table bit-identical to the
+oracle's model of src/sparseupdate.jl:97-129 (single-table update!) after one update, every
+case an independent draw.  Complements the targeted tests (chain paths, sizes, layouts)
+with shapes nobody picked by hand: batches at and around the chunk (256) and tile (4,096)
+boundaries, pools of 1, rows of 1."""
+import numpy as np
+import pytest
+import torch
+
+import embtab as et
+from embtab.tables import AbstractEmbeddingTable, Static, fused_update_path
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+class _ColPtr(AbstractEmbeddingTable):
+    def __init__(self, dense, rng):
+        R, D = dense.shape
+        self.R, self.D = R, D
+        self.pitch = D + 16 // dense.element_size()
+        self.perm = torch.from_numpy(rng.permutation(R)).to(DEV)
+        self.pool = torch.zeros((R, self.pitch), dtype=dense.dtype, device=DEV)
+        self.pool[self.perm, :D] = dense
+        self.lookup_type = Static(D)
+
+    def size(self):
+        return (self.D, self.R)
+
+    def columnpointers(self):
+        es = self.pool.element_size()
+        return self.pool.data_ptr() + self.perm.cpu().numpy().astype(np.int64) * self.pitch * es
+
+    def example(self):
+        return self.pool[0:1, :self.D]
+
+    def dense(self):
+        return self.pool[self.perm, :self.D]
+
+
+def _case(seed):
+    rng = np.random.default_rng(seed)
+    kind = ["f32", "f64", "f16", "f16acc", "bf16"][seed % 5]
+    storage = ["simple", "paged", "colptr"][(seed // 5) % 3]
+    R = int(rng.choice([1, 3, 17, 128, 129, 1000, 5000]))
+    D = int(rng.choice([16, 64, 128]))
+    P = int(rng.choice([1, 2, 7, 20]))
+    B = int(rng.choice([1, 255, 256, 257, 4095, 4096, 4097, 20000]))
+    zipf = bool(rng.integers(0, 2))
+    return rng, kind, storage, R, D, P, B, zipf
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_random_default_update_vs_oracle(oracle, seed):
+    from oracle import f32_to_bf16
+
+    rng, kind, storage, R, D, P, B, zipf = _case(seed)
+    x = rng.standard_normal((R, D)).astype(np.float32)
+    d = rng.standard_normal((B, D)).astype(np.float32)
+    if kind == "bf16":
+        base, delta = f32_to_bf16(x), f32_to_bf16(d)
+    else:
+        dt = {"f32": np.float32, "f64": np.float64, "f16": np.float16, "f16acc": np.float16}[kind]
+        base, delta = x.astype(dt), d.astype(dt)
+    if zipf and R > 1:
+        u = rng.random((B, P))
+        a1 = 1.0 - 1.05
+        I = np.floor(((float(R) ** a1 - 1.0) * u + 1.0) ** (1.0 / a1)).clip(1, R).astype(np.int64)
+        I = rng.permutation(R)[I - 1] + 1
+    else:
+        I = rng.integers(1, R + 1, (B, P))
+    if P == 1 and seed % 2:
+        I = I[:, 0].copy()  # vector indices
+    tdev = torch.from_numpy(base).to(DEV)
+    ddev = torch.from_numpy(delta).to(DEV)
+    if kind == "bf16":
+        tdev, ddev = tdev.view(torch.bfloat16), ddev.view(torch.bfloat16)
+    if storage == "simple":
+        A = et.SimpleEmbedding(tdev, Static(D))
+    elif storage == "paged":
+        A = et.SplitEmbedding(tdev, int(rng.integers(1, max(2, R) + 1)))
+    else:
+        A = _ColPtr(tdev, rng)
+    g = et.SparseEmbeddingUpdate(A.lookup_type, ddev, torch.from_numpy(I).to(DEV))
+    et.update_(et.Descent(0.1), A, g, f16_fp32_acc=kind == "f16acc")
+    ref = base.copy()
+    oracle.sgd(ref, delta, I, 0.1, fused=fused_update_path(A), bf16=kind == "bf16",
+               f16_fp32_acc=kind == "f16acc")
+    got = A.data if storage == "simple" else (A.to_dense() if storage == "paged" else A.dense())
+    got = (got.view(torch.int16) if kind in ("bf16", "f16", "f16acc") else got).cpu().numpy()
+    assert got.tobytes() == ref.view(got.dtype).tobytes(), (kind, storage, R, D, P, B, zipf)
+    assert et.check_errors() == 0
+
+
+@pytest.mark.parametrize("seed", range(100, 120))
+def test_random_multi_table_update_vs_oracle(oracle, seed):
+    """The multi-table update! (src/sparseupdate.jl:199-238) over 2-6 tables of one element
+    type with random storages, rows, dims and pools, sharing one Preallocation-strided gradient
+    (k prepended rows), in one pipeline; indexers filled; every table bit-identical to the
+    oracle's per-table update of its slice (fused path: Float32 eta; tables whose column
+    exceeds 512 bytes take the generic path with the Float64 eta, as the reference)."""
+    from oracle import f32_to_bf16
+
+    rng = np.random.default_rng(seed)
+    kind = ["f32", "f64", "f16", "bf16"][seed % 4]
+    n = int(rng.integers(2, 7))
+    B = int(rng.choice([300, 4097, 30000]))
+    k = int(rng.choice([0, 1, 4]))
+    rows = [int(rng.choice([2, 50, 128, 900, 6000])) for _ in range(n)]
+    dims = [int(rng.choice([32, 64, 128])) for _ in range(n)]
+    pools = [int(rng.choice([1, 5, 20])) for _ in range(n)]
+    ld = k + sum(dims)
+    dt = {"f32": np.float32, "f64": np.float64, "f16": np.float16}.get(kind)
+    conv = (lambda a: f32_to_bf16(a)) if kind == "bf16" else (lambda a: a.astype(dt))
+    hs = [conv(rng.standard_normal((r, d)).astype(np.float32)) for r, d in zip(rows, dims)]
+    delta = conv(rng.standard_normal((B, ld)).astype(np.float32))
+    hidx = [rng.integers(1, r + 1, (B, p)) for r, p in zip(rows, pools)]
+    for t in range(n):  # a hot column in some tables (a chain)
+        if rng.integers(0, 2):
+            hidx[t][:, 0] = 1
+    ddev = torch.from_numpy(delta).to(DEV)
+    if kind == "bf16":
+        ddev = ddev.view(torch.bfloat16)
+    tabs = []
+    for t in range(n):
+        x = torch.from_numpy(hs[t]).to(DEV)
+        if kind == "bf16":
+            x = x.view(torch.bfloat16)
+        st = int(rng.integers(0, 3))
+        tabs.append(et.SimpleEmbedding(x, Static(dims[t])) if st == 0 else
+                    et.SplitEmbedding(x, int(rng.integers(1, rows[t] + 1))) if st == 1 else
+                    _ColPtr(x, rng))
+    offs = np.cumsum([k] + dims[:-1]).tolist()
+    grads = [et.SparseEmbeddingUpdate(A.lookup_type, ddev[:, o:o + d], torch.from_numpy(i).to(DEV))
+             for A, o, d, i in zip(tabs, offs, dims, hidx)]
+    ixs = [et.Indexer() for _ in tabs]
+    et.update_(et.Descent(0.1), tabs, grads, ixs)
+    refs = [h.copy() for h in hs]
+    oracle.sgd_multi(refs, delta, hidx, 0.1, [fused_update_path(A) for A in tabs], num_splits=4,
+                     nthreads=4, delta_offsets=offs, bf16=kind == "bf16")
+    for t, A in enumerate(tabs):
+        got = A.data if isinstance(A, et.SimpleEmbedding) else (
+            A.to_dense() if isinstance(A, et.SplitEmbedding) else A.dense())
+        got = (got.view(torch.int16) if kind in ("bf16", "f16") else got).cpu().numpy()
+        assert got.tobytes() == refs[t].view(got.dtype).tobytes(), (kind, t, rows, dims, pools, B)
+        cum, mp = oracle.index_build(hidx[t], rows[t])
+        assert np.array_equal(ixs[t].cumulative.cpu().numpy(), cum)
+        assert np.array_equal(ixs[t].map.cpu().numpy(), mp)
+    assert et.check_errors() == 0
