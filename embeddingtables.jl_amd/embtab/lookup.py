@@ -146,11 +146,11 @@ def lookup_(dst: torch.Tensor, A: AbstractEmbeddingTable, I: torch.Tensor,
                                      dst.data_ptr(), _ld(dst), flags,
                                      _lib.stream_handle(dst.device))
     elif I.dim() == 1:
-        rc = L.et_gather(_lib.et_dtype(dst), A.columnpointer(1), A.ld, R, D, I.data_ptr(), B,
+        rc = L.et_gather(_lib.et_dtype(dst), table, A.ld, R, D, I.data_ptr(), B,
                          dst.data_ptr(), _ld(dst), flags, _lib.stream_handle(dst.device))
     else:
         P = int(I.shape[1])
-        rc = L.et_pooled_sum(_lib.et_dtype(dst), A.columnpointer(1), A.ld, R, D, I.data_ptr(), P,
+        rc = L.et_pooled_sum(_lib.et_dtype(dst), table, A.ld, R, D, I.data_ptr(), P,
                              _ld(I), B, dst.data_ptr(), _ld(dst), flags,
                              _lib.stream_handle(dst.device))
     _lib.check(rc)

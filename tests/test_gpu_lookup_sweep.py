@@ -1,0 +1,101 @@
+"""A seeded random sweep of the lookup paths against the oracle: `lookup` (vector gather and
+matrix pooled sum, src/lookup.jl:51-165) and the Preallocation `maplookup` (:305-371) over
+random tables — storage (contiguous, paged with a random page size, device column pointers),
+element type (Float32, Float64, Float16 in Julia's arithmetic or with Float32 sums, BFloat16,
+Int32, Int64), rows, dims (vector-path and odd ones), pools, batches, prepended rows — every
+output bit-identical to the oracle, every case an independent draw."""
+import numpy as np
+import pytest
+import torch
+
+import embtab as et
+from embtab.tables import AbstractEmbeddingTable, Static
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+KINDS = ["f32", "f64", "f16", "f16acc", "bf16", "i32", "i64"]
+
+
+class _ColPtr(AbstractEmbeddingTable):
+    def __init__(self, dense, rng):
+        R, D = dense.shape
+        self.R, self.D = R, D
+        es = dense.element_size()
+        self.pitch = D + 16 // es
+        self.perm = torch.from_numpy(rng.permutation(R)).to(DEV)
+        self.pool = torch.zeros((R, self.pitch), dtype=dense.dtype, device=DEV)
+        self.pool[self.perm, :D] = dense
+        self.lookup_type = Static(D)
+
+    def size(self):
+        return (self.D, self.R)
+
+    def columnpointers(self):
+        es = self.pool.element_size()
+        return self.pool.data_ptr() + self.perm.cpu().numpy().astype(np.int64) * self.pitch * es
+
+    def example(self):
+        return self.pool[0:1, :self.D]
+
+
+def _host_table(rng, kind, R, D):
+    from oracle import f32_to_bf16
+
+    if kind in ("i32", "i64"):
+        return rng.integers(-1000, 1000, (R, D)).astype(np.int32 if kind == "i32" else np.int64)
+    x = rng.standard_normal((R, D)).astype(np.float32)
+    if kind == "bf16":
+        return f32_to_bf16(x)
+    return x.astype({"f32": np.float32, "f64": np.float64, "f16": np.float16,
+                     "f16acc": np.float16}[kind])
+
+
+def _dev_table(h, kind, storage, rng):
+    x = torch.from_numpy(h).to(DEV)
+    if kind == "bf16":
+        x = x.view(torch.bfloat16)
+    D = h.shape[1]
+    if storage == "simple":
+        return et.SimpleEmbedding(x, Static(D))
+    if storage == "paged":
+        return et.SplitEmbedding(x, int(rng.integers(1, h.shape[0] + 1)))
+    return _ColPtr(x, rng)
+
+
+def _bits(t, kind):
+    if kind in ("bf16", "f16", "f16acc"):
+        t = t.view(torch.int16)
+    return t.cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_lookup_and_maplookup_vs_oracle(oracle, seed):
+    rng = np.random.default_rng(1000 + seed)
+    kind = KINDS[seed % len(KINDS)]
+    bf16, acc = kind == "bf16", kind == "f16acc"
+    n = int(rng.integers(1, 5))
+    B = int(rng.choice([1, 7, 128, 1000, 4097]))
+    P = int(rng.choice([1, 3, 20, 33]))
+    k = int(rng.choice([0, 1, 16]))
+    rows = [int(rng.choice([1, 5, 300, 3000])) for _ in range(n)]
+    dims = [int(rng.choice([5, 16, 20, 64, 96, 128, 256])) for _ in range(n)]
+    hs = [_host_table(rng, kind, r, d) for r, d in zip(rows, dims)]
+    tabs = [_dev_table(h, kind, ["simple", "paged", "colptr"][int(rng.integers(0, 3))], rng)
+            for h in hs]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    # lookup: pooled sum of table 0 (matrix indices) and the gather (vector indices)
+    # (lookup sums Float16 in Julia's Float16 arithmetic; maplookup below takes the option)
+    got = et.lookup(tabs[0], torch.from_numpy(hidx[0]).to(DEV))
+    ref = oracle.pooled_sum(hs[0], hidx[0], bf16=bf16)
+    assert _bits(got, kind) == np.ascontiguousarray(ref).view(ref.dtype).tobytes(), "pooled"
+    v = hidx[0][:, 0].copy()
+    got = et.lookup(tabs[0], torch.from_numpy(v).to(DEV))
+    assert _bits(got, kind) == np.ascontiguousarray(oracle.gather(hs[0], v, bf16=bf16)).tobytes()
+    # the Preallocation maplookup over every table (one fused launch)
+    y = et.maplookup(et.PreallocationStrategy(k), tabs, [torch.from_numpy(i).to(DEV) for i in hidx],
+                     f16_fp32_acc=acc)
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=k, f16_fp32_acc=acc, bf16=bf16)
+    got = y.view(torch.int16) if kind in ("bf16", "f16", "f16acc") else y
+    got = got.cpu().numpy()[:, k:]
+    assert got.tobytes() == np.ascontiguousarray(ref[:, k:]).view(got.dtype).tobytes(), "maplookup"
+    assert et.check_errors() == 0
