@@ -99,3 +99,50 @@ def test_random_lookup_and_maplookup_vs_oracle(oracle, seed):
     got = got.cpu().numpy()[:, k:]
     assert got.tobytes() == np.ascontiguousarray(ref[:, k:]).view(got.dtype).tobytes(), "maplookup"
     assert et.check_errors() == 0
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_sharded_step_loopback_vs_oracle(oracle, seed):
+    """The native sharded Preallocation step (csrc/et_shard.cpp) on N loopback ranks of one
+    process, random shapes: 2-8 ranks, table-wise (count- or size-dealt) or feature-wise
+    plans, all-gather in 1-5 pipelined chunks or all-to-all, odd batches, prepended rows —
+    every rank's rows equal the unsharded oracle concat (src/lookup.jl:316-371)."""
+    from test_gpu_loopback import Ranks, run_ranks
+
+    from embtab.sharding import ShardPlan, piece_table
+
+    rng = np.random.default_rng(2000 + seed)
+    world = int(rng.integers(2, 9))
+    n = int(rng.integers(world, 3 * world + 1))
+    dims = [int(rng.choice([32, 64, 96, 128])) for _ in range(n)]
+    rows = [int(rng.choice([3, 100, 2000, 30000])) for _ in range(n)]
+    B = int(rng.integers(world, 3000))
+    P = int(rng.choice([1, 8, 20]))
+    k = int(rng.choice([0, 3]))
+    planner = ["tablewise", "tablewise_sizes", "featurewise"][seed % 3]
+    exchange = "alltoall" if seed % 4 == 3 else "allgather"
+    chunks = 1 if exchange == "alltoall" else int(rng.integers(1, 6))
+    hs = [rng.random((r, d), dtype=np.float32) for r, d in zip(rows, dims)]
+    hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    full = [et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(h.shape[1])) for h in hs]
+    didx = [torch.from_numpy(i).to(DEV) for i in hidx]
+    ref = oracle.maplookup_prealloc(hs, hidx, prependrows=k)
+    plan = (ShardPlan.featurewise(dims, world, k) if planner == "featurewise" else
+            ShardPlan.tablewise(dims, world, k, sizes=rows if planner == "tablewise_sizes" else None))
+    ranks = Ranks(plan, world, B, exchange, chunks)
+    try:
+        outs = []
+        for st in ranks.steps:
+            lo, hi = st._native.lo, st._native.hi
+            outs.append(torch.full((hi - lo, plan.ld), -3.0, dtype=torch.float32, device=DEV))
+        tabs = [[piece_table(full[p.table], p) for p in plan.pieces[r]] for r in range(world)]
+        idxs = [[didx[p.table] for p in plan.pieces[r]] for r in range(world)]
+        run_ranks(world, lambda r: ranks.steps[r](tabs[r], idxs[r], outs[r]))
+        torch.cuda.synchronize()
+        for r, st in enumerate(ranks.steps):
+            lo, hi = st._native.lo, st._native.hi
+            got = outs[r].cpu().numpy()
+            assert got[:, k:].tobytes() == np.ascontiguousarray(ref[lo:hi, k:]).tobytes(), (
+                seed, r, world, planner, exchange, chunks)
+    finally:
+        ranks.close()
