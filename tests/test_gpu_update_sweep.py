@@ -150,3 +150,62 @@ def test_random_multi_table_update_vs_oracle(oracle, seed):
         assert np.array_equal(ixs[t].cumulative.cpu().numpy(), cum)
         assert np.array_equal(ixs[t].map.cpu().numpy(), mp)
     assert et.check_errors() == 0
+
+
+@pytest.mark.parametrize("seed", range(200, 212))
+def test_random_indexer_views_and_phased_update_vs_oracle(oracle, seed):
+    """Random shapes through the reference's lower-level entry points: index!(Indexer, ...)
+    then update!(table, grad, IndexerView(ix, num_splits, s), alpha) for every split
+    (src/utils.jl:320-338, src/sparseupdate.jl:46-154; partition exactness as
+    test/update.jl:90-120), and the two-phase multi-table update (PhasedUpdate: index while
+    the gradient is produced, then apply) — both equal to the oracle, bit for bit."""
+    rng = np.random.default_rng(seed)
+    R = int(rng.choice([2, 40, 700, 5000]))
+    D = int(rng.choice([16, 64, 128, 200]))
+    B = int(rng.choice([1, 100, 4096, 9000]))
+    P = int(rng.choice([1, 6, 20]))
+    dtype = np.float64 if seed % 3 == 0 else np.float32
+    h = rng.standard_normal((R, D)).astype(dtype)
+    delta = rng.standard_normal((B, D)).astype(dtype)
+    I = rng.integers(1, R + 1, (B, P))
+    if rng.integers(0, 2):
+        I[:, 0] = 1  # a hot column
+    storage = ["simple", "paged", "colptr"][seed % 3]
+    x = torch.from_numpy(h).to(DEV)
+    A = (et.SimpleEmbedding(x, Static(D)) if storage == "simple" else
+         et.SplitEmbedding(x, int(rng.integers(1, R + 1))) if storage == "paged" else
+         _ColPtr(x, rng))
+    g = et.SparseEmbeddingUpdate(A.lookup_type, torch.from_numpy(delta).to(DEV),
+                                 torch.from_numpy(I).to(DEV))
+    ix = et.index_(et.Indexer(), g.indices, R)
+    ns = int(rng.integers(1, 6))
+    alpha = float(rng.choice([0.1, 0.5, 1.0]))
+    for s in range(1, ns + 1):
+        et.update_(A, g, et.IndexerView(ix, ns, s), alpha)
+    ref = h.copy()
+    oracle.sgd(ref, delta, I, alpha, fused=fused_update_path(A))
+
+    def dense(T):
+        return (T.data if isinstance(T, et.SimpleEmbedding) else
+                T.to_dense() if isinstance(T, et.SplitEmbedding) else T.dense())
+
+    assert dense(A).cpu().numpy().tobytes() == ref.tobytes(), ("views", R, D, B, P, ns, storage)
+    # the phased multi-table update of this table and a second one
+    h2 = rng.standard_normal((int(rng.choice([3, 900])), D)).astype(dtype)
+    I2 = rng.integers(1, h2.shape[0] + 1, (B, P))
+    A2 = et.SimpleEmbedding(torch.from_numpy(h2).to(DEV), Static(D))
+    dd = torch.zeros((B, 2 * D), dtype=torch.float64 if dtype == np.float64 else torch.float32,
+                     device=DEV)
+    grads = [et.SparseEmbeddingUpdate(A.lookup_type, dd[:, :D], g.indices),
+             et.SparseEmbeddingUpdate(A2.lookup_type, dd[:, D:], torch.from_numpy(I2).to(DEV))]
+    pu = et.PhasedUpdate([A, A2], grads)
+    pu.index_()
+    d2 = rng.standard_normal((B, 2 * D)).astype(dtype)
+    dd.copy_(torch.from_numpy(d2))  # the gradient arrives after the index phase
+    pu.update_(et.Descent(0.1))
+    refs = [ref, h2.copy()]
+    oracle.sgd_multi(refs, d2, [I, I2], 0.1, [fused_update_path(A), fused_update_path(A2)],
+                     delta_offsets=[0, D])
+    assert dense(A).cpu().numpy().tobytes() == refs[0].tobytes(), "phased 0"
+    assert A2.data.cpu().numpy().tobytes() == refs[1].tobytes(), "phased 1"
+    assert et.check_errors() == 0
