@@ -34,6 +34,72 @@ namespace et {
     } while (0)
 
 // ---------------------------------------------------------------------------------------
+// Recycled events and side streams.  A caller's stream that waited on one of our events
+// (the sharded step's join, a loopback rank's copies) may be a pooled stream the caller
+// reuses long after the step or the group is gone (torch hands out 32 pooled streams per
+// priority round-robin); destroying the event then was followed, tests later, by a
+// segmentation fault inside hipGraphLaunch of a capture on such a stream (full GPU suite,
+// round 6).  So the runtime never destroys the events and streams it hands to callers'
+// streams: et_sharded_destroy / et_comm_destroy return them to a per-device free list that
+// later steps and groups take from (bounded by the peak number alive at once).
+// ---------------------------------------------------------------------------------------
+struct Recycler {
+    std::mutex mu;
+    std::vector<std::pair<int, hipEvent_t>> events;
+    std::vector<std::pair<int, hipStream_t>> streams;
+};
+inline Recycler& recycler() {
+    static Recycler* r = new Recycler();  // never destroyed: in use until process exit
+    return *r;
+}
+inline hipError_t take_event(hipEvent_t* e) {
+    int dev = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err != hipSuccess) return err;
+    {
+        Recycler& r = recycler();
+        std::lock_guard<std::mutex> lk(r.mu);
+        for (size_t i = 0; i < r.events.size(); ++i)
+            if (r.events[i].first == dev) {
+                *e = r.events[i].second;
+                r.events[i] = r.events.back();
+                r.events.pop_back();
+                return hipSuccess;
+            }
+    }
+    return hipEventCreateWithFlags(e, hipEventDisableTiming);
+}
+inline void give_event(hipEvent_t e, int dev) {
+    if (!e) return;
+    Recycler& r = recycler();
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.events.emplace_back(dev, e);
+}
+inline hipError_t take_stream(hipStream_t* s) {
+    int dev = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err != hipSuccess) return err;
+    {
+        Recycler& r = recycler();
+        std::lock_guard<std::mutex> lk(r.mu);
+        for (size_t i = 0; i < r.streams.size(); ++i)
+            if (r.streams[i].first == dev) {
+                *s = r.streams[i].second;
+                r.streams[i] = r.streams.back();
+                r.streams.pop_back();
+                return hipSuccess;
+            }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+inline void give_stream(hipStream_t s, int dev) {
+    if (!s) return;
+    Recycler& r = recycler();
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.streams.emplace_back(dev, s);
+}
+
+// ---------------------------------------------------------------------------------------
 // Loopback communicator: N simulated ranks of ONE process (one host thread per rank, all
 // on the current GPU).  It lets the world > 1 code of the sharded step — gathered-chunk
 // offsets, all-to-all splits, the side-stream event pipeline — run unchanged without N
@@ -58,6 +124,7 @@ struct LoopGroup {
     uint64_t gen = 0;
     std::vector<LoopPost> post;
     std::vector<hipEvent_t> ready, done;  // per rank: its sends produced / its copies done
+    int device = 0;                       // where the events were made
     int err = 0;                          // first failure of the current collective
 
     bool broken = false;                  // a rank gave up waiting: the group is unusable
@@ -451,15 +518,15 @@ extern "C" int et_comm_loopback(void** comms, int32_t nranks) {
     g->post.resize(nranks);
     g->ready.assign(nranks, nullptr);
     g->done.assign(nranks, nullptr);
-    hipError_t e = hipSuccess;
+    hipError_t e = hipGetDevice(&g->device);
     for (int r = 0; r < nranks && e == hipSuccess; ++r) {
-        e = hipEventCreateWithFlags(&g->ready[r], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&g->done[r], hipEventDisableTiming);
+        e = et::take_event(&g->ready[r]);
+        if (e == hipSuccess) e = et::take_event(&g->done[r]);
     }
     if (e != hipSuccess) {
         for (int r = 0; r < nranks; ++r) {
-            if (g->ready[r]) (void)hipEventDestroy(g->ready[r]);
-            if (g->done[r]) (void)hipEventDestroy(g->done[r]);
+            et::give_event(g->ready[r], g->device);
+            et::give_event(g->done[r], g->device);
         }
         delete g;
         return et::fail(ET_ERR_HIP, "event creation failed: %s", hipGetErrorString(e));
@@ -481,10 +548,10 @@ extern "C" int et_comm_destroy(void* comm) {
             et::LoopComm* c = (et::LoopComm*)comm;
             et::LoopGroup* g = c->g;
             delete c;
-            if (--g->live == 0) {  // the last rank of the group frees it
+            if (--g->live == 0) {  // the last rank of the group frees it (events recycled)
                 for (int r = 0; r < g->n; ++r) {
-                    (void)hipEventDestroy(g->ready[r]);
-                    (void)hipEventDestroy(g->done[r]);
+                    et::give_event(g->ready[r], g->device);
+                    et::give_event(g->done[r], g->device);
                 }
                 delete g;
             }
@@ -584,12 +651,11 @@ extern "C" int et_sharded_create(void** handle, void* comm, int32_t world, int32
                                       s->slab_ld * es, 256);
     hipError_t e = hipGetDevice(&s->device);
     if (e == hipSuccess && s->chunks > 1) {
-        e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
+        e = et::take_stream(&s->side);
         s->ev.assign(s->chunks, nullptr);
-        for (int c = 0; e == hipSuccess && c < s->chunks; ++c)
-            e = hipEventCreateWithFlags(&s->ev[c], hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_out, hipEventDisableTiming);
+        for (int c = 0; e == hipSuccess && c < s->chunks; ++c) e = et::take_event(&s->ev[c]);
+        if (e == hipSuccess) e = et::take_event(&s->ev_in);
+        if (e == hipSuccess) e = et::take_event(&s->ev_out);
     }
     if (e != hipSuccess) {
         et_sharded_destroy(s);
@@ -769,11 +835,11 @@ extern "C" int et_sharded_destroy(void* handle) {
     if (!s) return ET_OK;
     int dev = -1;
     if (hipGetDevice(&dev) == hipSuccess && dev != s->device) (void)hipSetDevice(s->device);
-    for (hipEvent_t e : s->ev)
-        if (e) (void)hipEventDestroy(e);
-    if (s->ev_in) (void)hipEventDestroy(s->ev_in);
-    if (s->ev_out) (void)hipEventDestroy(s->ev_out);
-    if (s->side) (void)hipStreamDestroy(s->side);
+    // recycled, not destroyed (see Recycler): callers' streams may have waited on them
+    for (hipEvent_t e : s->ev) et::give_event(e, s->device);
+    et::give_event(s->ev_in, s->device);
+    et::give_event(s->ev_out, s->device);
+    et::give_stream(s->side, s->device);
     if (dev >= 0 && dev != s->device) (void)hipSetDevice(dev);
     delete s;
     return ET_OK;

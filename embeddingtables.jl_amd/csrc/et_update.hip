@@ -1350,7 +1350,6 @@ __global__ __launch_bounds__(256) void k_chain_tcount(UpdatePack pack, int ntabl
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
         const ChainTile c = chain_tile(trec, tile);
         const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
-        const uint32_t sh = chain_shift(pack.d[c.t].batch);
         const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
         stage_bags(bags, vals, c.ss, c.se, c.a, occ_off, pool);
         __syncthreads();
@@ -3112,7 +3111,7 @@ constexpr uint32_t kExactChunk = ET_SGD_CHUNK;
 // but every choice timed slow in the first-streams layouts, though the same choice fixed from
 // the start ran at full speed: the cost depends on the queues' history, not only on their
 // order).  Kept: the side streams at the least priority (below), which leaves the caller's
-// normal-priority queues to the caller and makes a shared pipe cost +20% instead of +30%.
+// normal-priority queues to the caller and makes a shared pipe cost +16% instead of +30%.
 struct SideStreams {
     static constexpr int kN = 4;  // early chains, regular chains, early hot columns, work
     static constexpr int kEc = 0, kReg = 1, kEh = 2, kWork = 3;
@@ -3140,7 +3139,7 @@ inline SideStreams* side_streams() {
         // The side streams take the LEAST priority (round 6): their queues then come from the
         // low-priority pool, not from the caller's normal-priority queues, and when one does
         // share the caller's pipe the pipe favours the caller's dispatches — config 4 with
-        // one or two streams opened before the library's first call: 4.37-4.46 ms instead of
+        // one or two streams opened before the library's first call: 4.28-4.46 ms instead of
         // 4.72-4.81 at the greatest priority; 3.66-3.71 ms in every other layout measured
         // (profiles/r06/queue_layout/).  ET_SIDE_HIGH=1 (experiment builds): the greatest.
         const int prio = ET_KNOB("ET_SIDE_HIGH", 0) ? greatest : least;

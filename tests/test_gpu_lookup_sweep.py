@@ -83,21 +83,47 @@ def test_random_lookup_and_maplookup_vs_oracle(oracle, seed):
     tabs = [_dev_table(h, kind, ["simple", "paged", "colptr"][int(rng.integers(0, 3))], rng)
             for h in hs]
     hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+    tdt = tabs[0].dtype
+
+    def guarded(rows_, cols_):
+        """A (rows_, cols_) destination inside a canary-filled buffer: one guard row above and
+        below, 7 guard columns on each side (row stride cols_ + 14), so any write outside
+        the destination shows up as a changed canary."""
+        buf = torch.full((rows_ + 2, cols_ + 14), 0, dtype=tdt, device=DEV)
+        buf.view(torch.uint8).fill_(0xA5)
+        return buf, buf[1:rows_ + 1, 7:7 + cols_]
+
+    def canaries_intact(buf, rows_, cols_):
+        b = buf.view(torch.uint8).view(rows_ + 2, -1)
+        es = buf.element_size()
+        inner = torch.zeros_like(b, dtype=torch.bool)
+        inner[1:rows_ + 1, 7 * es:(7 + cols_) * es] = True
+        return bool((b[~inner] == 0xA5).all())
+
     # lookup: pooled sum of table 0 (matrix indices) and the gather (vector indices)
     # (lookup sums Float16 in Julia's Float16 arithmetic; maplookup below takes the option)
-    got = et.lookup(tabs[0], torch.from_numpy(hidx[0]).to(DEV))
+    buf, dst = guarded(B, dims[0])
+    got = et.lookup_(dst, tabs[0], torch.from_numpy(hidx[0]).to(DEV))
     ref = oracle.pooled_sum(hs[0], hidx[0], bf16=bf16)
-    assert _bits(got, kind) == np.ascontiguousarray(ref).view(ref.dtype).tobytes(), "pooled"
+    assert _bits(got.contiguous(), kind) == np.ascontiguousarray(ref).view(ref.dtype).tobytes(), "pooled"
+    assert canaries_intact(buf, B, dims[0]), "pooled: write outside the destination"
     v = hidx[0][:, 0].copy()
-    got = et.lookup(tabs[0], torch.from_numpy(v).to(DEV))
-    assert _bits(got, kind) == np.ascontiguousarray(oracle.gather(hs[0], v, bf16=bf16)).tobytes()
+    buf, dst = guarded(B, dims[0])
+    got = et.lookup_(dst, tabs[0], torch.from_numpy(v).to(DEV))
+    assert _bits(got.contiguous(), kind) == np.ascontiguousarray(
+        oracle.gather(hs[0], v, bf16=bf16)).tobytes()
+    assert canaries_intact(buf, B, dims[0]), "gather: write outside the destination"
     # the Preallocation maplookup over every table (one fused launch)
-    y = et.maplookup(et.PreallocationStrategy(k), tabs, [torch.from_numpy(i).to(DEV) for i in hidx],
-                     f16_fp32_acc=acc)
+    ld = k + sum(dims)
+    buf, dst = guarded(B, ld)
+    y = et.maplookup_(et.PreallocationStrategy(k), dst, tabs,
+                      [torch.from_numpy(i).to(DEV) for i in hidx], f16_fp32_acc=acc)
     ref = oracle.maplookup_prealloc(hs, hidx, prependrows=k, f16_fp32_acc=acc, bf16=bf16)
-    got = y.view(torch.int16) if kind in ("bf16", "f16", "f16acc") else y
+    got = y.contiguous()
+    got = got.view(torch.int16) if kind in ("bf16", "f16", "f16acc") else got
     got = got.cpu().numpy()[:, k:]
     assert got.tobytes() == np.ascontiguousarray(ref[:, k:]).view(got.dtype).tobytes(), "maplookup"
+    assert canaries_intact(buf, B, ld), "maplookup: write outside the destination"
     assert et.check_errors() == 0
 
 
