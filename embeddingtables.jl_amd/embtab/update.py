@@ -112,8 +112,13 @@ _ws_cache: dict = {}
 
 
 def _workspace(nbytes: int, device, key: str) -> torch.Tensor:
-    """A cached device byte buffer of at least ``nbytes`` (allocated outside the C call)."""
-    k = (key, str(device))
+    """A cached device byte buffer of at least ``nbytes`` (allocated outside the C call), one
+    per (key, device, stream): the calls that share a workspace are then ordered on their
+    stream, while calls on two streams — from two threads, or one thread alternating
+    streams — never share one (round 6: a shared workspace let two threads' concurrent
+    updates corrupt each other's keys and fault the GPU).  Allocated on that stream (the
+    current one), so the caching allocator orders its reuse after the stream's work."""
+    k = (key, str(device), _lib.stream_handle(device))
     buf = _ws_cache.get(k)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)

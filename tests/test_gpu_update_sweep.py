@@ -209,3 +209,118 @@ def test_random_indexer_views_and_phased_update_vs_oracle(oracle, seed):
     assert dense(A).cpu().numpy().tobytes() == refs[0].tobytes(), "phased 0"
     assert A2.data.cpu().numpy().tobytes() == refs[1].tobytes(), "phased 1"
     assert et.check_errors() == 0
+
+
+@pytest.mark.parametrize("seed", range(300, 306))
+def test_random_step_captured_in_a_graph_replays_eager_bits(oracle, seed):
+    """A random training step — Preallocation maplookup of 2-5 tables of mixed storage, the
+    rrule pullback, the multi-table default (exact) update with indexers — captured once in a
+    HIP graph after an eager warm-up and replayed twice on fresh tables: bit-identical to the
+    same two steps run eagerly (every launch stream-ordered, no host synchronisation inside)."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2, 6))
+    B = int(rng.choice([64, 1000, 4096]))
+    P = int(rng.choice([1, 8, 20]))
+    rows = [int(rng.choice([3, 128, 2000])) for _ in range(n)]
+    dims = [int(rng.choice([32, 64, 128])) for _ in range(n)]
+    kinds = [int(rng.integers(0, 3)) for _ in range(n)]
+    hs = [rng.standard_normal((r, d)).astype(np.float32) for r, d in zip(rows, dims)]
+    idx = [torch.from_numpy(rng.integers(1, r + 1, (B, P))).to(DEV) for r in rows]
+    dy = torch.from_numpy(rng.standard_normal((B, sum(dims))).astype(np.float32)).to(DEV)
+
+    def make():
+        out = []
+        for h, kd in zip(hs, kinds):
+            x = torch.from_numpy(h).to(DEV)
+            out.append(et.SimpleEmbedding(x, Static(x.shape[1])) if kd == 0 else
+                       et.SplitEmbedding(x, int(rng.integers(1, x.shape[0] + 1))) if kd == 1 else
+                       _ColPtr(x, np.random.default_rng(seed)))
+        return out
+
+    def dense(T):
+        return (T.data if isinstance(T, et.SimpleEmbedding) else
+                T.to_dense() if isinstance(T, et.SplitEmbedding) else T.dense())
+
+    def step(tabs, dst):
+        et.maplookup_(et.PreallocationStrategy(0), dst, tabs, idx)
+        offs = np.cumsum([0] + dims[:-1]).tolist()
+        grads = [et.SparseEmbeddingUpdate(t.lookup_type, dy[:, o:o + d], i)
+                 for t, o, d, i in zip(tabs, offs, dims, idx)]
+        et.update_(et.Descent(0.05), tabs, grads, [et.Indexer() for _ in tabs])
+
+    eager = make()
+    out_e = torch.empty((B, sum(dims)), dtype=torch.float32, device=DEV)
+    step(eager, out_e)
+    step(eager, out_e)
+    graphed = make()
+    for t in graphed:  # a column-pointer table's device pointer array is built (and uploaded)
+        t.device_table()  # on first use: outside the capture, as any host-to-device copy
+    out_g = torch.empty_like(out_e)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up outside the capture (workspaces)
+        step(make(), torch.empty_like(out_e))
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step(graphed, out_g)
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out_g, out_e)
+    for a, b in zip(graphed, eager):
+        assert torch.equal(dense(a), dense(b))
+    assert et.check_errors() == 0
+
+
+def test_concurrent_exact_updates_from_two_threads(oracle):
+    """Two host threads, each with its own stream and tables, run default (exact) multi-table
+    updates 6 times at once: the library's shared side streams and fork/join events serialise
+    the calls' side work correctly, and every table equals the oracle's six serial updates."""
+    import threading
+
+    rng = np.random.default_rng(400)
+    B, P, D = 2048, 20, 64
+    cases = []
+    for _ in range(2):
+        rows = [3, 500, 20000]
+        hs = [rng.standard_normal((r, D)).astype(np.float32) for r in rows]
+        hidx = [rng.integers(1, r + 1, (B, P)) for r in rows]
+        for i in hidx:
+            i[:, :2] = 1  # a chain in every table
+        delta = rng.standard_normal((B, 3 * D)).astype(np.float32)
+        cases.append((rows, hs, hidx, delta))
+    results, errs = [None, None], []
+
+    def body(c):
+        try:
+            rows, hs, hidx, delta = cases[c]
+            st = torch.cuda.Stream(DEV)
+            with torch.cuda.stream(st):
+                tabs = [et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(D)) for h in hs]
+                dd = torch.from_numpy(delta).to(DEV)
+                grads = [et.SparseEmbeddingUpdate(t.lookup_type, dd[:, k * D:(k + 1) * D],
+                                                  torch.from_numpy(i).to(DEV))
+                         for k, (t, i) in enumerate(zip(tabs, hidx))]
+                for _ in range(6):
+                    et.update_(et.Descent(0.1), tabs, grads, None)
+                results[c] = [t.data.cpu().numpy() for t in tabs]
+            st.synchronize()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=body, args=(c,)) for c in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=180)
+    assert not errs, errs
+    assert not any(t.is_alive() for t in th)
+    for c in range(2):
+        rows, hs, hidx, delta = cases[c]
+        for k in range(3):
+            w = hs[k].copy()
+            for _ in range(6):
+                oracle.sgd(w, np.ascontiguousarray(delta[:, k * D:(k + 1) * D]), hidx[k], 0.1,
+                           fused=True)
+            assert results[c][k].tobytes() == w.tobytes(), (c, k)
