@@ -339,12 +339,15 @@ end
 _fused(::HipTable{Static{N},T}) where {N,T} = N * sizeof(T) <= 512
 _fused(::HipTable) = false
 
-const WORKSPACE = Ref{Any}(nothing)
-function _workspace(nbytes)
-    ws = WORKSPACE[]
+# Update workspaces, one per (stream, slot): calls that share one are ordered on their stream,
+# so setting STREAM[] to another stream never lets two in-flight calls share a workspace.
+const WORKSPACES = Dict{Tuple{Ptr{Cvoid},Int},Any}()
+function _workspace(nbytes, slot::Int = -1)
+    k = (stream(), slot)
+    ws = get(WORKSPACES, k, nothing)
     if ws === nothing || length(ws) < nbytes
         ws = HipArray{UInt8}(undef, nbytes)
-        WORKSPACE[] = ws
+        WORKSPACES[k] = ws
     end
     return ws
 end
@@ -508,7 +511,6 @@ end
 #    occurrence per step, 272 MB and 34 M insertions at BASELINE config 4).
 # One Indexer object at several positions ends up holding the LAST one's indices, as the
 # reference's sequential index! calls leave it, so only its last position is snapshotted.
-const WORKSPACES = Dict{Int,Any}()
 function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
                  grads::AbstractVector{<:SparseEmbeddingUpdate},
                  indexers::AbstractVector{<:AbstractIndexer}, ::Val{Nontemporal} = Val(true);
@@ -531,12 +533,7 @@ function update!(opt::Flux.Descent, tables::AbstractVector{<:HipTable},
             nb = Ref{Int64}(0)
             check(ccall((:et_sgd_workspace_size, libembtab), Cint,
                         (Ptr{UpdateDesc}, Int32, Ref{Int64}), descs, length(descs), nb))
-            k = length(calls)
-            ws = get(WORKSPACES, k, nothing)
-            if ws === nothing || length(ws) < nb[]
-                ws = HipArray{UInt8}(undef, nb[])
-                WORKSPACES[k] = ws
-            end
+            ws = _workspace(nb[], length(calls))
             push!(calls, (T, descs, flags, ws, Ptr{Int64}[snap[i] for i in chunk]))
         end
     end
