@@ -99,3 +99,25 @@ def test_split_embedding_host_logic():
         et.SplitEmbedding(data, 0)
     with pytest.raises(et.ArgumentError):
         et.lookup(A, torch.tensor([1, 2, 3]))  # no CPU fallback for paged tables either
+
+
+def test_update_workspaces_are_per_stream(monkeypatch):
+    """Round 6: the update's cached workspace is per (key, device, stream) — two streams never
+    share one (concurrent updates on two streams corrupted a shared one), one stream reuses its
+    own, and a larger request replaces it (CPU stand-in for the device and the streams)."""
+    from embtab import _lib, update
+
+    cur = {"s": 1}
+    monkeypatch.setattr(_lib, "stream_handle", lambda device=None: cur["s"])
+    monkeypatch.setattr(update, "_ws_cache", {})
+    dev = torch.device("cpu")
+    a = update._workspace(1000, dev, "sgd")
+    assert update._workspace(900, dev, "sgd") is a
+    cur["s"] = 2
+    b = update._workspace(1000, dev, "sgd")
+    assert b is not a and b.data_ptr() != a.data_ptr()
+    cur["s"] = 1
+    assert update._workspace(1000, dev, "sgd") is a
+    c = update._workspace(5000, dev, "sgd")
+    assert c is not a and c.numel() >= 5000
+    assert update._workspace(1000, dev, "index") is not c
