@@ -324,3 +324,30 @@ def test_concurrent_exact_updates_from_two_threads(oracle):
                 oracle.sgd(w, np.ascontiguousarray(delta[:, k * D:(k + 1) * D]), hidx[k], 0.1,
                            fused=True)
             assert results[c][k].tobytes() == w.tobytes(), (c, k)
+
+
+def test_empty_batches_through_every_entry_point(oracle):
+    """Batches of zero bags (and pools of zero) through maplookup (Preallocation), the rrule
+    pullback, the single- and multi-table update with indexers, and the phased update: no launch
+    faults, outputs have the right (empty) shapes, tables are unchanged, and the indexers are
+    the reference's empty Indexer (cumulative = [(0, 1)])."""
+    rng = np.random.default_rng(500)
+    hs = [rng.standard_normal((r, 64)).astype(np.float32) for r in (5, 300)]
+    tabs = [et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(64)) for h in hs]
+    for shape in ((0, 20), (0,), (7, 0)):
+        I = [torch.zeros(shape, dtype=torch.int64, device=DEV) for _ in tabs]
+        y, back = et.rrule(et.maplookup, et.PreallocationStrategy(2), tabs, I)
+        assert tuple(y.shape) == (shape[0], 2 + 128)
+        grads = back(torch.zeros_like(y))[2]
+        ixs = [et.Indexer(), et.Indexer()]
+        et.update_(et.Descent(0.1), tabs, grads, ixs)
+        for k in range(2):
+            et.update_(et.Descent(0.1), tabs[k], grads[k], et.Indexer())
+        pu = et.PhasedUpdate(tabs, grads)
+        pu.index_()
+        pu.update_(et.Descent(0.1))
+        torch.cuda.synchronize()
+        for A, h, ix in zip(tabs, hs, ixs):
+            assert A.data.cpu().numpy().tobytes() == h.tobytes()
+            assert ix.cumulative.cpu().numpy().tolist() == [[0, 1]]
+    assert et.check_errors() == 0
