@@ -351,3 +351,84 @@ def test_empty_batches_through_every_entry_point(oracle):
             assert A.data.cpu().numpy().tobytes() == h.tobytes()
             assert ix.cumulative.cpu().numpy().tolist() == [[0, 1]]
     assert et.check_errors() == 0
+
+
+def test_concurrent_lookups_and_updates_on_three_streams(oracle):
+    """Three host threads at once, each on its own stream and tables: Preallocation maplookups
+    (per-XCD queue blocks), multi-table exact updates with indexers (side streams, snapshots),
+    single-table lookups + updates of a paged table — each thread's results equal the oracle's
+    serial model of its own calls."""
+    import threading
+
+    rng = np.random.default_rng(600)
+    B, P, D = 1024, 20, 64
+    # thread 0: maplookups
+    hA = [rng.standard_normal((r, D)).astype(np.float32) for r in (7, 900, 5000)]
+    iA = [rng.integers(1, r + 1, (B, P)) for r in (7, 900, 5000)]
+    # thread 1: multi-table updates
+    hB = [rng.standard_normal((r, D)).astype(np.float32) for r in (3, 2000)]
+    iB = [rng.integers(1, r + 1, (B, P)) for r in (3, 2000)]
+    dB = rng.standard_normal((B, 2 * D)).astype(np.float32)
+    # thread 2: lookups + single-table updates of a paged table
+    hC = rng.standard_normal((777, D)).astype(np.float32)
+    iC = rng.integers(1, 778, (B, P))
+    dC = rng.standard_normal((B, D)).astype(np.float32)
+    out, errs = {}, []
+
+    def t0():
+        tabs = [et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(D)) for h in hA]
+        idx = [torch.from_numpy(i).to(DEV) for i in iA]
+        ys = [et.maplookup(et.PreallocationStrategy(0), tabs, idx) for _ in range(8)]
+        out[0] = [y.cpu().numpy() for y in ys]
+
+    def t1():
+        tabs = [et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(D)) for h in hB]
+        dd = torch.from_numpy(dB).to(DEV)
+        grads = [et.SparseEmbeddingUpdate(t.lookup_type, dd[:, k * D:(k + 1) * D],
+                                          torch.from_numpy(i).to(DEV))
+                 for k, (t, i) in enumerate(zip(tabs, iB))]
+        ixs = [et.Indexer(), et.Indexer()]
+        for _ in range(4):
+            et.update_(et.Descent(0.1), tabs, grads, ixs)
+        out[1] = ([t.data.cpu().numpy() for t in tabs], [ix.map.cpu().numpy() for ix in ixs])
+
+    def t2():
+        A = et.SplitEmbedding(torch.from_numpy(hC).to(DEV), 50)
+        I = torch.from_numpy(iC).to(DEV)
+        g = et.SparseEmbeddingUpdate(A.lookup_type, torch.from_numpy(dC).to(DEV), I)
+        ys = []
+        for _ in range(4):
+            ys.append(et.lookup(A, I).cpu().numpy())
+            et.update_(et.Descent(0.1), A, g)
+        out[2] = (ys, A.to_dense().cpu().numpy())
+
+    def run(fn):
+        try:
+            st = torch.cuda.Stream(DEV)
+            with torch.cuda.stream(st):
+                fn()
+            st.synchronize()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(f,)) for f in (t0, t1, t2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=180)
+    assert not errs, errs
+    assert not any(t.is_alive() for t in th)
+    ref = np.ascontiguousarray(oracle.maplookup_prealloc(hA, iA, prependrows=0)).tobytes()
+    assert all(y.tobytes() == ref for y in out[0])
+    w = [h.copy() for h in hB]
+    for _ in range(4):
+        for k in range(2):
+            oracle.sgd(w[k], np.ascontiguousarray(dB[:, k * D:(k + 1) * D]), iB[k], 0.1, fused=True)
+    for k in range(2):
+        assert out[1][0][k].tobytes() == w[k].tobytes()
+        assert np.array_equal(out[1][1][k], oracle.index_build(iB[k], hB[k].shape[0])[1])
+    wc = hC.copy()
+    for it in range(4):
+        assert out[2][0][it].tobytes() == oracle.pooled_sum(wc, iC).tobytes()
+        oracle.sgd(wc, dC, iC, 0.1, fused=True)
+    assert out[2][1].tobytes() == wc.tobytes()
