@@ -1142,8 +1142,33 @@ __device__ __forceinline__ uint32_t chain_entry(uint32_t r, uint32_t bag, uint32
     return r << sh | bag;
 }
 
+// Whether a chain of a table with this gradient can take the hand-scheduled Float32 loops
+// (et_chain_asm.h, chain_walk_quad): their gradient addresses are 32-bit byte offsets in one
+// range-checked buffer — bag * ld * 4 + 4 * feature from 24-bit factors, and a padding entry
+// (bag = batch) must land past the range to load +0 — so (batch + 1) * ld * 4 stays below
+// 2^32 and ld below 2^22.  Any other chain takes chain_walk_wide (64-bit addresses).
+__host__ __device__ inline bool chain_asm_ok(int64_t batch, int64_t ld) {
+    return batch < kChainNarrowBatch && ld < (1ll << 22) &&
+           (uint64_t)(batch + 1) * (uint64_t)ld * 4u < (1ull << 32);
+}
+
+// The streamed loop's gradient stride in bytes for a chain at S of a table with this gradient,
+// 0 when the chain does not take it (the index phase then writes no offsets / masks).
+__host__ __device__ inline uint32_t chain_stream_ld4(int64_t batch, int64_t ld, uint32_t S) {
+    return S >= (uint32_t)kChainStreamMinS && chain_asm_ok(batch, ld) ? (uint32_t)ld * 4u : 0u;
+}
+
 struct ChainCol {
     uint32_t key, e0, ngr, S;  // S == 0: no chain (out-of-range occurrences)
+};
+
+// A chain list's entries and, for the streamed Float32 loop (S >= kChainStreamMinS on a
+// table chain_asm_ok admits, et_chain_asm.h chain_walk_stream), per entry its gradient byte
+// offset bag * ld * 4 and its lane mask (2^r - 1 in each 16-lane row), at the same index.
+struct ChainEnt {
+    uint32_t* ent;
+    uint32_t* off;
+    uint64_t* msk;
 };
 
 __device__ __forceinline__ uint32_t cdiv_u32(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
@@ -1345,6 +1370,9 @@ __global__ __launch_bounds__(256) void k_chain_tcount(UpdatePack pack, int ntabl
                                                       uint32_t* __restrict__ tcnt) {
     __shared__ uint32_t bags[kChainLds];
     __shared__ uint32_t red[4][5];
+#ifdef ET_PLAN_PRIO
+    __builtin_amdgcn_s_setprio(ET_PLAN_PRIO);
+#endif
     const uint32_t M = counters[kCntM], T = counters[kCntT];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
@@ -1455,12 +1483,29 @@ __global__ __launch_bounds__(kPlanThreads) void k_chain_plan(const uint32_t* __r
 }
 
 // One run of r adds of delta column `bag` as ceil(r/S) entries (S adds each, the last
-// one the remainder).
-__device__ __forceinline__ void chain_put(uint32_t* __restrict__ ent, uint32_t at, uint32_t i,
+// one the remainder); with `ld4` (nonzero: the chain takes the streamed loop) also the
+// entry's gradient offset and lane mask.
+__device__ __forceinline__ uint64_t chain_lane_mask(uint32_t adds) {
+    return (uint64_t)((1u << adds) - 1u) * 0x0001000100010001ull;
+}
+__device__ __forceinline__ void chain_put(const ChainEnt& ce, uint32_t at, uint32_t i,
                                           uint32_t k, uint32_t r, uint32_t S, uint32_t bag,
-                                          uint32_t sh) {
+                                          uint32_t sh, uint32_t ld4) {
     const uint32_t adds = i + 1 < k ? S : r - S * (k - 1);
-    ent[at] = chain_entry(adds, bag, sh);
+    ce.ent[at] = chain_entry(adds, bag, sh);
+    if (ld4) {
+        ce.off[at] = bag * ld4;
+        ce.msk[at] = chain_lane_mask(adds);
+    }
+}
+// A padding entry (no adds, bag = batch: its loads return +0).
+__device__ __forceinline__ void chain_pad(const ChainEnt& ce, uint32_t at, uint32_t batch,
+                                          uint32_t sh, uint32_t ld4) {
+    ce.ent[at] = chain_entry(0u, batch, sh);
+    if (ld4) {
+        ce.off[at] = batch * ld4;
+        ce.msk[at] = 0ull;
+    }
 }
 
 // Index phase 5, per tile: the entries of the runs that start in it (after the entries
@@ -1480,11 +1525,14 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
                                                     const uint32_t* __restrict__ cnt,
                                                     const uint2* __restrict__ info,
                                                     const uint32_t* __restrict__ e0s,
-                                                    uint32_t* __restrict__ ent,
+                                                    ChainEnt ce,
                                                     ChainCol* __restrict__ chains) {
     __shared__ uint32_t bags[kChainLds];
     __shared__ uint32_t rl[kChainTile];  // run length at a head, 0 elsewhere
     __shared__ uint32_t red[2][4];
+#ifdef ET_PLAN_PRIO
+    __builtin_amdgcn_s_setprio(ET_PLAN_PRIO);
+#endif
     const uint32_t M = counters[kCntM], T = counters[kCntT];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
@@ -1493,6 +1541,7 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
         const uint32_t S = in.x, kS = (uint32_t)(__ffs((int)S) - 1);
         const uint32_t occ_off = pack.occ_off[c.t], pool = (uint32_t)pack.d[c.t].pool;
         const uint32_t sh = chain_shift(pack.d[c.t].batch);
+        const uint32_t ld4 = chain_stream_ld4(pack.d[c.t].batch, pack.d[c.t].ld_delta, S);
         const uint32_t n = c.a + kChainTile < c.se ? kChainTile : c.se - c.a;
         stage_bags(bags, vals, c.ss, c.se, c.a, occ_off, pool);
         __syncthreads();
@@ -1518,13 +1567,13 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
             const uint32_t r = rl[j0 + j];
             if (r == 0u) continue;
             const uint32_t k = cdiv_u32(r, S), bag = bags[j0 + j + 1];
-            for (uint32_t i = 0; i < k; ++i) chain_put(ent, at + i, i, k, r, S, bag, sh);
+            for (uint32_t i = 0; i < k; ++i) chain_put(ce, at + i, i, k, r, S, bag, sh, ld4);
             at += k;
         }
         if (c.ti + 1 == c.nt) {
             const uint32_t e0 = e0s[c.m], P = cnt[c.m];
-            const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[c.t].batch, sh);
-            for (uint32_t i = e0 + in.y + threadIdx.x; i < e0 + P; i += 256) ent[i] = pad;
+            for (uint32_t i = e0 + in.y + threadIdx.x; i < e0 + P; i += 256)
+                chain_pad(ce, i, (uint32_t)pack.d[c.t].batch, sh, ld4);
             if (threadIdx.x == 0)
                 chains[c.m] = ChainCol{keys[c.ss], e0, (P - kChainPad) / kChainGroup, S};
         }
@@ -1540,7 +1589,7 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
                                                      const uint32_t* __restrict__ counters,
                                                      const uint32_t* __restrict__ cnt,
                                                      const uint2* __restrict__ info,
-                                                     uint32_t* __restrict__ ent,
+                                                     ChainEnt ce,
                                                      const ChainCol* __restrict__ chains,
                                                      const uint32_t* __restrict__ order) {
     const uint32_t M = counters[kCntM];
@@ -1554,16 +1603,19 @@ __global__ __launch_bounds__(256) void k_chain_check(UpdatePack pack, int ntable
         const int t = table_of_key(pack, ntables, c.key);
         const uint64_t lim = (uint64_t)pack.d[t].batch;
         const uint32_t sh = chain_shift(pack.d[t].batch), bm = (1u << sh) - 1u;
+        const uint32_t ld4 = chain_stream_ld4(pack.d[t].batch, pack.d[t].ld_delta, c.S);
         uint32_t bad = 0, real = 0, pad_then_real = 0;
         if (P != c.ngr * kChainGroup + kChainPad || c.S != info[m].x) bad = 1;
         for (uint32_t i = lane; i < P; i += 64) {
-            const uint32_t e = ent[c.e0 + i], r = e >> sh;
-            const bool ok = ((uint64_t)(e & bm) < lim || (r == 0u && (e & bm) == lim)) &&
-                            r <= c.S;
+            const uint32_t e = ce.ent[c.e0 + i], r = e >> sh;
+            bool ok = ((uint64_t)(e & bm) < lim || (r == 0u && (e & bm) == lim)) && r <= c.S;
+            if (ld4)  // the streamed loop's offset and mask say the same as the entry
+                ok = ok && ce.off[c.e0 + i] == (e & bm) * ld4 &&
+                     ce.msk[c.e0 + i] == (r ? chain_lane_mask(r) : 0ull);
             // a bad entry becomes a padding entry (bag = batch: its range-checked load
             // returns +0), so the debug pass reports the violation without adding
             // gradient column 0 in its place (maskless S = 1 and quad walks add every entry)
-            if (!ok) ent[c.e0 + i] = chain_entry(0u, (uint32_t)lim, sh);
+            if (!ok) chain_pad(ce, c.e0 + i, (uint32_t)lim, sh, ld4);
             bad += ok ? 0u : 1u;
             real += (ok && r > 0u) ? 1u : 0u;
             pad_then_real += (ok && r > 0u && i >= info[m].y) ? 1u : 0u;
@@ -1832,7 +1884,7 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
                                                  uint32_t* __restrict__ nocc,
                                                  uint2* __restrict__ info,
                                                  ChainCol* __restrict__ chains,
-                                                 uint32_t* __restrict__ ent,
+                                                 ChainEnt ce,
                                                  uint32_t* __restrict__ counters, int kmax,
                                                  const uint32_t* __restrict__ cand) {
     const int lane = threadIdx.x & 63;
@@ -1881,8 +1933,9 @@ __global__ __launch_bounds__(256) void k_ec_plan(UpdatePack pack, EcList ec, uin
         if (b < nblk) boff[ec.cb0[e] + c * nblk + b] = carry + ex;
         carry += wave_sum_u32(x);
     }
-    const uint32_t pad = chain_entry(0u, (uint32_t)pack.d[t].batch, 24u);  // ec_table: batch <= 2^20
-    for (uint32_t i = e0 + E + (uint32_t)lane; i < e0 + P; i += 64) ent[i] = pad;
+    const uint32_t ld4 = chain_stream_ld4(pack.d[t].batch, pack.d[t].ld_delta, S);
+    for (uint32_t i = e0 + E + (uint32_t)lane; i < e0 + P; i += 64)  // ec_table: batch <= 2^20
+        chain_pad(ce, i, (uint32_t)pack.d[t].batch, 24u, ld4);
 }
 
 // EC step 3 (one workgroup): the cost order of the EC columns — costliest first, so the
@@ -1922,7 +1975,7 @@ __global__ __launch_bounds__(1024) void k_ec_order(EcList ec, const uint2* __res
 __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
                                                  const uint32_t* __restrict__ boff,
                                                  const uint2* __restrict__ info,
-                                                 uint32_t* __restrict__ ent,
+                                                 ChainEnt ce,
                                                  const uint32_t* __restrict__ cand) {
     extern __shared__ __attribute__((aligned(16))) uint8_t hist[];  // kEcBags x ec_rs(ec)
     __shared__ uint32_t psum[kEcBags];
@@ -1941,12 +1994,13 @@ __global__ __launch_bounds__(256) void k_ec_emit(UpdatePack pack, EcList ec,
     __syncthreads();
     if (!S) return;  // no barrier below
     uint32_t at = boff[ec.cb0[e] + q.c * nblk + blk];
+    const uint32_t ld4 = chain_stream_ld4(d.batch, d.ld_delta, S);
     for (uint32_t p = 0; p < q.p; ++p) at += psum[p * q.R + q.c];
     for (uint32_t i = q.b0; i < q.b1; ++i) {
         const uint32_t r = hist[i * q.RS + q.c];
         const uint32_t k = cdiv_u32(r, S);
         const uint32_t bag = blk * kEcBags + i;
-        for (uint32_t j = 0; j < k; ++j) chain_put(ent, at + j, j, k, r, S, bag, 24u);
+        for (uint32_t j = 0; j < k; ++j) chain_put(ce, at + j, j, k, r, S, bag, 24u, ld4);
         at += k;
     }
 }
@@ -2055,15 +2109,6 @@ __device__ __forceinline__ float chain_walk_quad(const uint32_t* ent, uint32_t n
     return acc;
 }
 
-// Whether a chain of a table with this gradient can take the hand-scheduled Float32 loops
-// (et_chain_asm.h, chain_walk_quad): their gradient addresses are 32-bit byte offsets in one
-// range-checked buffer — bag * ld * 4 + 4 * feature from 24-bit factors, and a padding entry
-// (bag = batch) must land past the range to load +0 — so (batch + 1) * ld * 4 stays below
-// 2^32 and ld below 2^22.  Any other chain takes chain_walk_wide (64-bit addresses).
-__host__ __device__ inline bool chain_asm_ok(int64_t batch, int64_t ld) {
-    return batch < kChainNarrowBatch && ld < (1ll << 22) &&
-           (uint64_t)(batch + 1) * (uint64_t)ld * 4u < (1ull << 32);
-}
 
 // The serial sum of one chain over one 64-feature slice (lane = feature), with 64-bit
 // gradient addresses and any element type: the reference's loop (src/sparseupdate.jl:110-127,
@@ -2114,13 +2159,22 @@ __device__ __forceinline__ C chain_walk_wide(const uint32_t* ent, uint32_t ngr, 
 // (the quad walk, 16 features each); any other chain takes the whole slice in quarter 0
 // (the other quarters return at once).  T is the table and gradient type, C the
 // accumulator (sgd_apply_t).
+// A wave-uniform pointer as an SGPR pair (for the asm loops' "s" operands).
+template <typename P>
+__device__ __forceinline__ P* uniform_ptr(P* p) {
+    const uint64_t b = reinterpret_cast<uint64_t>(p);
+    return reinterpret_cast<P*>(
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b) |
+        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32)) << 32);
+}
+
 template <typename T, typename C, int MODE, bool NT>
 __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntables,
                                                const ChainCol* __restrict__ chains,
                                                const uint32_t* __restrict__ order,
-                                               const uint32_t* __restrict__ ent, int ns,
+                                               const ChainEnt& ce, int ns,
                                                C eta_c, double eta64, uint32_t it4,
-                                               uint32_t quad_min) {
+                                               uint32_t quad_min, bool stream) {
     constexpr bool kF32 = __is_same(T, float);
     const int lane = threadIdx.x & 63;
     const uint32_t quarter = it4 % (uint32_t)kQuadItems, it = it4 / (uint32_t)kQuadItems;
@@ -2139,10 +2193,7 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
     const T* delta = reinterpret_cast<const T*>(
         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)db) |
         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(db >> 32)) << 32);
-    const uint64_t eb = reinterpret_cast<uint64_t>(ent + c.e0);
-    const uint32_t* e = reinterpret_cast<const uint32_t*>(
-        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)eb) |
-        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(eb >> 32)) << 32);
+    const uint32_t* e = uniform_ptr(ce.ent + c.e0);
     if constexpr (kF32) {
         if (quad) {
             const int f0 = slice * 64 + (int)quarter * 16;
@@ -2170,7 +2221,15 @@ __device__ __forceinline__ void sgd_chain_item(const UpdatePack& pack, int ntabl
             // range batch * ld * 4 bytes: a padding entry (bag = batch) loads +0
             const uint32_t ld = (uint32_t)d.ld_delta;
             const i32x4 rs = chain_rsrc(delta, (uint32_t)d.batch * ld * 4u);
-            switch (c.S) {
+            if (stream && c.S >= (uint32_t)kChainStreamMinS) {
+                // the index phase wrote this chain's offsets and masks (chain_stream_ld4)
+                const uint32_t* off = uniform_ptr(ce.off + c.e0);
+                const uint64_t* msk = uniform_ptr(ce.msk + c.e0);
+                // (64 x loads in flight instead of 32 measured no faster: the hottest early
+                // chain 3.16 against 3.05 ms, gpurun_out/r06zf)
+                acc = c.S == 8u ? chain_walk_stream<8, 32>(off, msk, c.ngr, rs, 4u * fc, 0.0f)
+                                : chain_walk_stream<16, 32>(off, msk, c.ngr, rs, 4u * fc, 0.0f);
+            } else switch (c.S) {
                 case 1: acc = chain_walk_asm<1>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
                 case 2: acc = chain_walk_asm<2>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
                 case 4: acc = chain_walk_asm<4>(e, c.ngr, rs, 4u * fc, 4u * ld, 0.0f); break;
@@ -2214,8 +2273,12 @@ __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
                                             uint32_t* __restrict__ counters,
                                             const ChainCol* __restrict__ chains,
                                             const uint32_t* __restrict__ order,
-                                            const uint32_t* __restrict__ ent, int ns, C eta_c,
+                                            const ChainEnt& ce, int ns, C eta_c,
                                             double eta64, uint32_t quad_min, uint32_t list) {
+    // list: bits 0-7 the list (0 early, 1 regular, 2 early hot; timelines), bit 8 the streamed
+    // loop for S >= kChainStreamMinS (experiment builds can turn it off: ET_CHAIN_STREAM=0)
+    const bool stream = (list & 0x100u) != 0u;
+    list &= 0xffu;
     const int lane = threadIdx.x & 63;
     __builtin_amdgcn_s_setprio(3);
     const uint32_t items = counters[kCntM] * (uint32_t)ns * (uint32_t)kQuadItems;
@@ -2227,8 +2290,8 @@ __device__ __forceinline__ void chain_items(const UpdatePack& pack, int ntables,
 #ifdef ET_EXPERIMENTS
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        sgd_chain_item<T, C, MODE, NT>(pack, ntables, chains, order, ent, ns, eta_c, eta64, it,
-                                       quad_min);
+        sgd_chain_item<T, C, MODE, NT>(pack, ntables, chains, order, ce, ns, eta_c, eta64, it,
+                                       quad_min, stream);
 #ifdef ET_EXPERIMENTS
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
         const ChainCol c = chains[order[(it / (uint32_t)kQuadItems) / (uint32_t)ns]];
@@ -2253,9 +2316,9 @@ template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_sgd_chains(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
+    ChainEnt ce, int ns, C eta_c, double eta64, uint32_t quad_min,
     uint32_t list) {
-    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
+    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ce, ns, eta_c, eta64,
                                 quad_min, list);
 }
 
@@ -2266,9 +2329,9 @@ template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(512) void k_sgd_chains_w(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
+    ChainEnt ce, int ns, C eta_c, double eta64, uint32_t quad_min,
     uint32_t list) {
-    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
+    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ce, ns, eta_c, eta64,
                                 quad_min, list);
 }
 
@@ -2281,10 +2344,10 @@ template <typename T, typename C, int MODE, bool NT>
 __global__ __launch_bounds__(256) void k_sgd_chains_x(
     UpdatePack pack, int ntables, uint32_t* __restrict__ counters,
     const ChainCol* __restrict__ chains, const uint32_t* __restrict__ order,
-    const uint32_t* __restrict__ ent, int ns, C eta_c, double eta64, uint32_t quad_min,
+    ChainEnt ce, int ns, C eta_c, double eta64, uint32_t quad_min,
     uint32_t list) {
     asm volatile("v_accvgpr_write_b32 a255, 0" ::: "a255");
-    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ent, ns, eta_c, eta64,
+    chain_items<T, C, MODE, NT>(pack, ntables, counters, chains, order, ce, ns, eta_c, eta64,
                                 quad_min, list);
 }
 
@@ -2396,7 +2459,7 @@ struct UpdateWs {
     // exact Float32 mode: chain entries (aliasing `partials`: that mode has no partial
     // sums), per chain column (multi-chunk list slot) its descriptor, padded entry count,
     // (S, entries), entry offset, and the cost-ordered slot list
-    uint32_t* chain_ent;
+    ChainEnt chain_ent;
     ChainCol* chains;
     uint32_t *chain_cnt, *chain_e0, *chain_order;
     uint2* chain_info;
@@ -2409,7 +2472,8 @@ struct UpdateWs {
     // padded entry count, (S, entries), descriptor and cost order, their entries, and a
     // counter block (kCntM = EC columns) for the chain role
     struct EcWs {
-        uint32_t *stats, *boff, *cnt, *order, *ent, *counters, *nocc;
+        uint32_t *stats, *boff, *cnt, *order, *counters, *nocc;
+        ChainEnt ent;
         uint2* info;
         ChainCol* chains;
     };
@@ -2419,6 +2483,15 @@ struct UpdateWs {
 };
 
 inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+// The entries, offsets and masks of a chain list in one buffer of 16 * n bytes (n even).
+inline ChainEnt chain_ent_at(char* p, int64_t n) {
+    ChainEnt c;
+    c.ent = reinterpret_cast<uint32_t*>(p);
+    c.off = p ? c.ent + n : nullptr;
+    c.msk = p ? reinterpret_cast<uint64_t*>(p + 8 * n) : nullptr;
+    return c;
+}
 
 // Index-phase tiles of the chain columns: at most one partial tile per column plus the
 // full ones.
@@ -2463,9 +2536,11 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
     // 8 bytes per partial element: float (vector path / fp32 accumulators) or double; the
     // exact mode's chain entries (8 bytes, at most one per occurrence + padding) alias it
     const int64_t part_b = 8 * max_partials * (int64_t)(pdim > 0 ? pdim : 1);
-    const int64_t chain_b = 4 * (n + (int64_t)(kChainGroup + kChainPad) * mmax + 64);
+    // entries, offsets and masks (4 + 4 + 8 bytes) of up to one entry per occurrence + padding
+    const int64_t chain_n = (n + (int64_t)(kChainGroup + kChainPad) * mmax + 64 + 1) & ~int64_t(1);
+    const int64_t chain_b = 16 * chain_n;
     w.partials = (float*)take(part_b > chain_b ? part_b : chain_b);
-    w.chain_ent = (uint32_t*)w.partials;
+    w.chain_ent = chain_ent_at(reinterpret_cast<char*>(w.partials), chain_n);
     w.chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * mmax);
     w.chain_cnt = (uint32_t*)take(4 * mmax);
     w.chain_e0 = (uint32_t*)take(4 * mmax);
@@ -2487,7 +2562,8 @@ inline UpdateWs carve_update_ws(char* base, int64_t n, int pdim, uint32_t chunk,
         e.info = (uint2*)take(8 * M);
         e.chains = (ChainCol*)take((int64_t)sizeof(ChainCol) * M);
         e.counters = (uint32_t*)take(4 * kCntSlots);
-        e.ent = (uint32_t*)take(4 * (occ + (int64_t)(kChainGroup + kChainPad) * M + 64));
+        const int64_t cn = (occ + (int64_t)(kChainGroup + kChainPad) * M + 64 + 1) & ~int64_t(1);
+        e.ent = chain_ent_at(take(16 * cn), cn);
         return e;
     };
     w.ec = carve_ec(ec, ec_occ);
@@ -2728,8 +2804,9 @@ constexpr unsigned kExactGrid = 384;
 // k_sgd_chains on stream `s`: zero the item counter, at most `nb` workgroups.
 template <typename T, typename C, int MODE, bool NT>
 int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const ChainCol* chains,
-                  const uint32_t* order, const uint32_t* ent, int ns, C eta_c, double eta64,
+                  const uint32_t* order, const ChainEnt& ce, int ns, C eta_c, double eta64,
                   unsigned nb, hipStream_t s, bool excl, uint32_t list, bool wide = false) {
+    if (ET_KNOB("ET_CHAIN_STREAM", 1)) list |= 0x100u;
     // the quad walk for Float32 S = 1 chains of at least this many 64-entry groups (§9 "The
     // quad walk": every S = 1 chain 5.56 ms, >= 4 K / 16 K / 64 K / 128 K entries 5.20 / 4.99 /
     // 4.07-4.16 / 4.36 ms, none 4.48-4.52; profiles/r03/c/ab_quad_min.txt)
@@ -2749,20 +2826,20 @@ int launch_chains(const UpdatePack& pack, int ntables, uint32_t* counters, const
     ET_HIP_CHECK(hipMemsetAsync(counters + kCntNext, 0, 4, s));
     if (wide) {
         hipLaunchKernelGGL((k_sgd_chains_w<T, C, MODE, NT>), dim3(nb), dim3(512),
-                           kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
+                           kChainReserveLds, s, pack, ntables, counters, chains, order, ce, ns,
                            eta_c, eta64, quad_min, list);
         ET_LAUNCH_CHECK("k_sgd_chains_w");
         return ET_OK;
     }
     if (excl) {
         hipLaunchKernelGGL((k_sgd_chains_x<T, C, MODE, NT>), dim3(nb), dim3(256),
-                           kChainReserveLds, s, pack, ntables, counters, chains, order, ent, ns,
+                           kChainReserveLds, s, pack, ntables, counters, chains, order, ce, ns,
                            eta_c, eta64, quad_min, list);
         ET_LAUNCH_CHECK("k_sgd_chains_x");
         return ET_OK;
     }
     hipLaunchKernelGGL((k_sgd_chains<T, C, MODE, NT>), dim3(nb), dim3(256), kChainReserveLds, s,
-                       pack, ntables, counters, chains, order, ent, ns, eta_c, eta64, quad_min,
+                       pack, ntables, counters, chains, order, ce, ns, eta_c, eta64, quad_min,
                        list);
     ET_LAUNCH_CHECK("k_sgd_chains");
     return ET_OK;
