@@ -1120,12 +1120,17 @@ __global__ __launch_bounds__(256) void k_hot_combine(UpdatePack pack, HotList hl
 
 constexpr int kChainGroup = kChainAsmTrip;  // entries per trip of the asm loop
 constexpr int kChainPad = kChainAsmPad;     // readable entries past the last trip
-// Issue slots of one entry of a chain at S adds per entry, doubled (et_chain_asm.h:
-// readlane, address, load and half a wait, then S = 1: the add; S = 2, 4 (the 64-deep
-// loop): a second readlane, the mask's compare and select and S masked fmas; S = 8, 16
-// (the 32-deep loop): the mask and S masked fmas).
+// Issue slots of one entry of a chain at S adds per entry, doubled (et_chain_asm.h: S = 1:
+// readlane, address, load, half a wait and the add; S = 2, 4 (the 64-deep loop): two
+// readlanes, address, load, half a wait, the mask's compare and select and S masked fmas;
+// S = 8, 16 (the streamed loop): the mask's select, load, half a wait, 3/8 for the scalar
+// loads and S masked fmas).
 __host__ __device__ constexpr uint32_t chain_entry_cost2(uint32_t S) {
+#ifdef ET_COST_OLD
     return S <= 1u ? 9u : S <= 4u ? 2u * S + 13u : 2u * S + 11u;
+#else
+    return S <= 1u ? 9u : S <= 4u ? 2u * S + 13u : 2u * S + 6u;
+#endif
 }
 
 // A chain entry: r adds (r <= 16) of gradient column `bag`; padding is r = 0 at bag = batch

@@ -29,7 +29,7 @@ DEV = torch.device("cuda:0")
 CHUNK = _lib.ET_SGD_CHUNK          # a longer column is a chain in the exact mode
 EC_MAX_ROWS = 128                  # et_update.hip kEcMaxRows
 QUAD_MIN_ENTRIES = 1024 * 64       # kQuadMinGroups 64-entry groups
-COST2 = {0: 9, 1: 17, 2: 21, 3: 27, 4: 43}  # chain_entry_cost2(2^k)
+COST2 = {0: 9, 1: 17, 2: 21, 3: 22, 4: 38}  # chain_entry_cost2(2^k)
 
 
 class ColumnPointerTable(AbstractEmbeddingTable):
@@ -238,3 +238,44 @@ def test_exact_default_at_2_pow_24_bags(oracle):
     ref2 = x.cpu().numpy()
     oracle.sgd(ref2, delta[:n].cpu().numpy(), I[:n].cpu().numpy(), 0.1, fused=True)
     assert A2.data.cpu().numpy().tobytes() == ref2.tobytes()
+
+
+def test_streamed_loop_on_the_regular_list(oracle):
+    """The streamed chain loop (S = 8 / 16: per-entry gradient offsets and lane masks written
+    by the plan, et_chain_asm.h chain_walk_stream) on the REGULAR list — columns of tables
+    above the early-chain size with 257..20,000 occurrences and many adds per bag, walked by
+    the shared-SIMD chain kernel — for contiguous, paged and column-pointer tables, and beside
+    early chains of the same call: every table bit-identical to the oracle's serial update."""
+    Bb, P, D = 2048, 64, 128
+    spec = [(300, 0), (257, 7), (400, 1), (60, 0)]  # (rows, cols per page; 0 contiguous)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(607)
+    rng = np.random.default_rng(608)
+    tabs, idx, base = [], [], []
+    for R, cpp in spec:
+        x = rng.standard_normal((R, D)).astype(np.float32)
+        t = torch.from_numpy(x).to(DEV)
+        A = (et.SimpleEmbedding(t, Static(D)) if cpp == 0 else
+             et.SplitEmbedding(t, cpp) if cpp > 1 else ColumnPointerTable(t, D + 4, gen))
+        tabs.append(A)
+        base.append(x)
+        idx.append(_zipf(R, (Bb, P), gen))
+    d = rng.standard_normal((Bb, D * len(spec))).astype(np.float32)
+    dd = torch.from_numpy(d).to(DEV)
+    grads = [et.SparseEmbeddingUpdate(A.lookup_type, dd[:, k * D:(k + 1) * D], i)
+             for k, (A, i) in enumerate(zip(tabs, idx))]
+    et.update_(et.Descent(0.1), tabs, grads)  # default (exact) mode
+    torch.cuda.synchronize()
+    assert et.check_errors() == 0
+    streamed = 0
+    for k, ((R, _), A, I) in enumerate(zip(spec, tabs, idx)):
+        ref = base[k].copy()
+        oracle.sgd(ref, np.ascontiguousarray(d[:, k * D:(k + 1) * D]), I.cpu().numpy(), 0.1,
+                   fused=True)
+        got = A.data if isinstance(A, et.SimpleEmbedding) else _dense(A)
+        assert got.cpu().numpy().tobytes() == ref.tobytes(), (k, R)
+        if R > EC_MAX_ROWS:
+            counts = torch.bincount(I.view(-1), minlength=R + 1)[1:]
+            for c in torch.nonzero((counts > CHUNK) & (counts <= 20000)).view(-1).tolist():
+                streamed += _chain_shape(I, c + 1)[0] >= 8
+    assert streamed >= 3, streamed  # the regular list holds S >= 8 chains
