@@ -1375,9 +1375,6 @@ __global__ __launch_bounds__(256) void k_chain_tcount(UpdatePack pack, int ntabl
                                                       uint32_t* __restrict__ tcnt) {
     __shared__ uint32_t bags[kChainLds];
     __shared__ uint32_t red[4][5];
-#ifdef ET_PLAN_PRIO
-    __builtin_amdgcn_s_setprio(ET_PLAN_PRIO);
-#endif
     const uint32_t M = counters[kCntM], T = counters[kCntT];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
@@ -1535,9 +1532,6 @@ __global__ __launch_bounds__(256) void k_chain_emit(UpdatePack pack, int ntables
     __shared__ uint32_t bags[kChainLds];
     __shared__ uint32_t rl[kChainTile];  // run length at a head, 0 elsewhere
     __shared__ uint32_t red[2][4];
-#ifdef ET_PLAN_PRIO
-    __builtin_amdgcn_s_setprio(ET_PLAN_PRIO);
-#endif
     const uint32_t M = counters[kCntM], T = counters[kCntT];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t tile = blockIdx.x; tile < T; tile += gridDim.x) {
