@@ -279,3 +279,45 @@ def test_streamed_loop_on_the_regular_list(oracle):
             for c in torch.nonzero((counts > CHUNK) & (counts <= 20000)).view(-1).tolist():
                 streamed += _chain_shape(I, c + 1)[0] >= 8
     assert streamed >= 3, streamed  # the regular list holds S >= 8 chains
+
+
+@pytest.mark.parametrize("Bb", [16382, 16383])
+def test_chain_offsets_at_the_32_bit_boundary(oracle, Bb):
+    """Gradient offsets at the edge of the asm loops' 32-bit buffer range: a gradient with a
+    65,536-float leading dimension, so bag * ld * 4 passes 2^31 from bag 8,192 on.  At 16,382
+    bags (batch + 1) * ld * 4 < 2^32: the early (4 rows, S = 8) and regular (200 rows) chains
+    take the streamed and packed asm loops with offsets up to 2^32 - 2^18; at 16,383 bags they
+    do not fit and take the 64-bit walk (chain_asm_ok).  Both bit-identical to the oracle."""
+    ld, dim = 65536, 64
+    spec = [(4, 32), (200, 64), (60, 20)]  # (rows, pool)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(609)
+    rng = np.random.default_rng(610)
+    L = _lib.load()
+    s = _lib.stream_handle()
+    delta = torch.empty((Bb, ld), dtype=torch.float32, device=DEV)
+    _lib.check(L.et_fill_uniform(_lib.ET_F32, delta.data_ptr(), delta.numel(), 6110, 0, -1.0, 1.0,
+                                 s))
+    tabs, idx, base = [], [], []
+    for R, P in spec:
+        x = rng.standard_normal((R, dim)).astype(np.float32)
+        tabs.append(et.SimpleEmbedding(torch.from_numpy(x).to(DEV), Static(dim)))
+        base.append(x)
+        idx.append(_zipf(R, (Bb, P), gen))
+    grads = [et.SparseEmbeddingUpdate(A.lookup_type, delta[:, k * dim:(k + 1) * dim], i)
+             for k, (A, i) in enumerate(zip(tabs, idx))]
+    et.update_(et.Descent(0.1), tabs, grads)  # default (exact) mode
+    torch.cuda.synchronize()
+    assert et.check_errors() == 0
+    d = delta[:, :dim * len(spec)].cpu().numpy()
+    del delta, grads
+    torch.cuda.empty_cache()
+    shapes = set()
+    for k, ((R, _), A, I) in enumerate(zip(spec, tabs, idx)):
+        ref = base[k].copy()
+        oracle.sgd(ref, np.ascontiguousarray(d[:, k * dim:(k + 1) * dim]), I.cpu().numpy(), 0.1,
+                   fused=True)
+        assert A.data.cpu().numpy().tobytes() == ref.tobytes(), (Bb, k, R)
+        counts = torch.bincount(I.view(-1), minlength=R + 1)[1:]
+        shapes |= {_chain_shape(I, c + 1)[0] for c in torch.nonzero(counts > CHUNK).view(-1).tolist()}
+    assert {1, 8} <= shapes or {1, 16} <= shapes, shapes  # packed and streamed loops both ran
