@@ -12,7 +12,9 @@ Mirrors (darchr/EmbeddingTables.jl):
 """
 from __future__ import annotations
 
+import collections
 import ctypes
+import threading
 
 import torch
 
@@ -108,7 +110,9 @@ class Descent:
 
 # --- workspaces ------------------------------------------------------------------------------
 
-_ws_cache: dict = {}
+_ws_cache: "collections.OrderedDict" = collections.OrderedDict()
+_WS_STREAMS = 4  # cached workspaces per (key, device): the most recently used streams
+_ws_lock = threading.Lock()
 
 
 def _workspace(nbytes: int, device, key: str) -> torch.Tensor:
@@ -117,12 +121,20 @@ def _workspace(nbytes: int, device, key: str) -> torch.Tensor:
     stream, while calls on two streams — from two threads, or one thread alternating
     streams — never share one (round 6: a shared workspace let two threads' concurrent
     updates corrupt each other's keys and fault the GPU).  Allocated on that stream (the
-    current one), so the caching allocator orders its reuse after the stream's work."""
+    current one), so the caching allocator orders its reuse after the stream's work — which
+    also makes dropping one safe while its stream still runs: at most ``_WS_STREAMS`` streams
+    per (key, device) keep theirs, the least recently used is released (a program cycling
+    through the pool's streams would otherwise hold a config-4-sized buffer per stream)."""
     k = (key, str(device), _lib.stream_handle(device))
-    buf = _ws_cache.get(k)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
-        _ws_cache[k] = buf
+    with _ws_lock:
+        buf = _ws_cache.get(k)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            _ws_cache[k] = buf
+        _ws_cache.move_to_end(k)
+        same = [x for x in _ws_cache if x[:2] == k[:2]]
+        for x in same[:-_WS_STREAMS]:
+            del _ws_cache[x]
     return buf
 
 

@@ -340,14 +340,27 @@ _fused(::HipTable{Static{N},T}) where {N,T} = N * sizeof(T) <= 512
 _fused(::HipTable) = false
 
 # Update workspaces, one per (stream, slot): calls that share one are ordered on their stream,
-# so setting STREAM[] to another stream never lets two in-flight calls share a workspace.
+# so setting STREAM[] to another stream never lets two in-flight calls share a workspace.  At
+# most WS_STREAMS streams per slot keep theirs (least recently used first out, after its stream
+# drains), so a program cycling through many streams does not hold a workspace per stream.
 const WORKSPACES = Dict{Tuple{Ptr{Cvoid},Int},Any}()
+const WS_ORDER = Tuple{Ptr{Cvoid},Int}[]
+const WS_STREAMS = 4
 function _workspace(nbytes, slot::Int = -1)
     k = (stream(), slot)
     ws = get(WORKSPACES, k, nothing)
     if ws === nothing || length(ws) < nbytes
         ws = HipArray{UInt8}(undef, nbytes)
         WORKSPACES[k] = ws
+    end
+    filter!(!=(k), WS_ORDER)
+    push!(WS_ORDER, k)
+    same = filter(x -> x[2] == slot, WS_ORDER)
+    for x in same[1:end-min(WS_STREAMS, length(same))]
+        ccall((:hipStreamSynchronize, libhip), Cint, (Ptr{Cvoid},), x[1]) == 0 ||
+            error("hipStreamSynchronize failed")
+        delete!(WORKSPACES, x)
+        filter!(!=(x), WS_ORDER)
     end
     return ws
 end

@@ -1,6 +1,7 @@
 """Host-side mirror of the reference API that runs without a GPU: constructors
 (test/constructors.jl), dispatch rules, index containers, IndexerView ranges, and
 that the product path refuses to compute on the CPU (no silent fallback)."""
+import collections
 import pytest
 import torch
 
@@ -109,7 +110,7 @@ def test_update_workspaces_are_per_stream(monkeypatch):
 
     cur = {"s": 1}
     monkeypatch.setattr(_lib, "stream_handle", lambda device=None: cur["s"])
-    monkeypatch.setattr(update, "_ws_cache", {})
+    monkeypatch.setattr(update, "_ws_cache", collections.OrderedDict())
     dev = torch.device("cpu")
     a = update._workspace(1000, dev, "sgd")
     assert update._workspace(900, dev, "sgd") is a
@@ -121,3 +122,10 @@ def test_update_workspaces_are_per_stream(monkeypatch):
     c = update._workspace(5000, dev, "sgd")
     assert c is not a and c.numel() >= 5000
     assert update._workspace(1000, dev, "index") is not c
+    # bounded: only the _WS_STREAMS most recently used streams per (key, device) keep theirs
+    for st in range(10, 10 + update._WS_STREAMS):
+        cur["s"] = st
+        update._workspace(1000, dev, "sgd")
+    sgd = [k for k in update._ws_cache if k[0] == "sgd"]
+    assert len(sgd) == update._WS_STREAMS and (("sgd", "cpu", 1)) not in sgd
+    assert ("index", "cpu", 1) in update._ws_cache  # another key keeps its own
