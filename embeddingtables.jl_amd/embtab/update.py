@@ -113,6 +113,7 @@ class Descent:
 _ws_cache: "collections.OrderedDict" = collections.OrderedDict()
 _WS_STREAMS = 4  # cached workspaces per (key, device): the most recently used streams
 _ws_lock = threading.Lock()
+_ws_pinned: dict = {}  # workspaces a HIP graph captured: never released (graphs replay into them)
 
 
 def _workspace(nbytes: int, device, key: str) -> torch.Tensor:
@@ -125,6 +126,7 @@ def _workspace(nbytes: int, device, key: str) -> torch.Tensor:
     also makes dropping one safe while its stream still runs: at most ``_WS_STREAMS`` streams
     per (key, device) keep theirs, the least recently used is released (a program cycling
     through the pool's streams would otherwise hold a config-4-sized buffer per stream)."""
+    device = torch.device(device)
     k = (key, str(device), _lib.stream_handle(device))
     with _ws_lock:
         buf = _ws_cache.get(k)
@@ -132,6 +134,11 @@ def _workspace(nbytes: int, device, key: str) -> torch.Tensor:
             buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
             _ws_cache[k] = buf
         _ws_cache.move_to_end(k)
+        if device.type == "cuda":
+            with torch.cuda.device(device):
+                if torch.cuda.is_current_stream_capturing():
+                    # a captured graph replays into this buffer: it outlives the cache
+                    _ws_pinned[id(buf)] = buf
         same = [x for x in _ws_cache if x[:2] == k[:2]]
         for x in same[:-_WS_STREAMS]:
             del _ws_cache[x]

@@ -432,3 +432,46 @@ def test_concurrent_lookups_and_updates_on_three_streams(oracle):
         assert out[2][0][it].tobytes() == oracle.pooled_sum(wc, iC).tobytes()
         oracle.sgd(wc, dC, iC, 0.1, fused=True)
     assert out[2][1].tobytes() == wc.tobytes()
+
+
+def test_captured_update_survives_workspace_eviction(oracle):
+    """The host caches update workspaces for the 4 most recently used streams per key and
+    releases older ones; a workspace a HIP graph captured is pinned instead — the graph replays
+    into it.  Capture an exact update, then run eager updates from 6 other streams (evicting
+    every cached workspace) and churn the allocator, then replay: bit-identical to the oracle's
+    two serial updates."""
+    rng = np.random.default_rng(700)
+    B, P, D, R = 4096, 20, 64, 300
+    h = rng.standard_normal((R, D)).astype(np.float32)
+    hi = rng.integers(1, R + 1, (B, P))
+    hd = rng.standard_normal((B, D)).astype(np.float32)
+    A = et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(D))
+    g_up = et.SparseEmbeddingUpdate(A.lookup_type, torch.from_numpy(hd).to(DEV),
+                                    torch.from_numpy(hi).to(DEV))
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):  # warm-up outside the capture
+        W = et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(D))
+        et.update_(et.Descent(0.1), W, g_up)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        et.update_(et.Descent(0.1), A, g_up)
+    torch.cuda.synchronize()
+    other = et.SimpleEmbedding(torch.from_numpy(h).to(DEV), Static(D))
+    for _ in range(6):
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            et.update_(et.Descent(0.1), other, g_up)
+            junk = torch.full((B * P * 16,), 7, dtype=torch.int32, device=DEV)  # reuse freed blocks
+            del junk
+        st.synchronize()
+    A.data.copy_(torch.from_numpy(h).to(DEV))  # the capture ran nothing: start from h
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    ref = h.copy()
+    for _ in range(2):
+        oracle.sgd(ref, hd, hi, 0.1, fused=True)
+    assert A.data.cpu().numpy().tobytes() == ref.tobytes()
+    assert et.check_errors() == 0
